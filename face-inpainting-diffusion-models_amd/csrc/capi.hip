@@ -1,0 +1,150 @@
+// extern "C" entry points of libifd.so (declared in include/ifd.h).
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "unet.h"
+
+static_assert(sizeof(ifd_step_coeffs) == sizeof(ifd::StepCoeffs), "coefficient struct layout");
+
+namespace ifd {
+static thread_local std::string g_err;
+void set_error(const std::string& m) { g_err = m; }
+const char* get_error() { return g_err.c_str(); }
+}  // namespace ifd
+
+struct ifd_handle {
+  ifd::Model* model;
+};
+
+using ifd::set_error;
+
+extern "C" {
+
+const char* ifd_last_error(void) { return ifd::get_error(); }
+const char* ifd_version(void) { return "ifd 0.1 gfx950 fp32-mfma"; }
+
+int ifd_create(const ifd_config* cfg, ifd_handle** out) {
+  if (!cfg || !out) {
+    set_error("ifd_create: null argument");
+    return 2;
+  }
+  if (cfg->num_levels < 1 || cfg->num_levels > 8 || cfg->model_channels % 32 != 0 || cfg->in_channels > 16 ||
+      cfg->num_res_blocks < 1 || (cfg->image_size >> (cfg->num_levels - 1)) < 2 || cfg->out_channels > 32 ||
+      cfg->out_channels % 2 != 0) {
+    set_error("ifd_create: unsupported configuration");
+    return 2;
+  }
+  try {
+    *out = new ifd_handle{new ifd::Model(*cfg)};
+  } catch (const std::exception& e) {
+    set_error(std::string("ifd_create: ") + e.what());
+    return 1;
+  }
+  return 0;
+}
+
+void ifd_destroy(ifd_handle* h) {
+  if (!h) return;
+  delete h->model;
+  delete h;
+}
+
+int ifd_num_params(ifd_handle* h, int* n) {
+  if (!h || !n) { set_error("null argument"); return 2; }
+  *n = (int)h->model->params().size();
+  return 0;
+}
+
+int ifd_param_info(ifd_handle* h, int i, const char** name, int64_t* shape4, int* ndim) {
+  if (!h) { set_error("null handle"); return 2; }
+  const auto& ps = h->model->params();
+  if (i < 0 || i >= (int)ps.size()) { set_error("param index out of range"); return 2; }
+  if (name) *name = ps[i].name.c_str();
+  if (ndim) *ndim = (int)ps[i].shape.size();
+  if (shape4)
+    for (int k = 0; k < 4; ++k) shape4[k] = k < (int)ps[i].shape.size() ? ps[i].shape[k] : 1;
+  return 0;
+}
+
+int ifd_load_weights(ifd_handle* h, const char* name, const float* data, const int64_t* shape, int ndim) {
+  if (!h || !name || !data || !shape) { set_error("ifd_load_weights: null argument"); return 2; }
+  return h->model->load(name, data, shape, ndim);
+}
+
+int ifd_finalize(ifd_handle* h) {
+  if (!h) { set_error("null handle"); return 2; }
+  return h->model->finalize();
+}
+
+int ifd_memory(ifd_handle* h, int64_t* wb, int64_t* ws) {
+  if (!h) { set_error("null handle"); return 2; }
+  if (wb) *wb = h->model->weight_bytes();
+  if (ws) *ws = h->model->workspace_bytes();
+  return 0;
+}
+
+int ifd_unet_forward(ifd_handle* h, const float* x, const float* masked_image, const float* mask, const int64_t* t,
+                     int64_t B, int H, int W, float* out6, void* stream) {
+  if (!h || !x || !masked_image || !mask || !t || !out6) { set_error("ifd_unet_forward: null argument"); return 2; }
+  return h->model->forward(x, masked_image, mask, 0, t, (int)B, H, W, ifd::EPI_NCHW, out6, nullptr, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+static int step_common(ifd_handle* h, int epi, const int64_t* t, int64_t B, int H, int W, float* img, const float* gt,
+                       const float* mask, const float* noise, const float* known, const ifd_step_coeffs* c,
+                       void* stream) {
+  if (!h || !t || !img || !gt || !mask || !c) { set_error("ifd step: null argument"); return 2; }
+  if (c->inject && !known) { set_error("ifd step: inject requires known noise"); return 2; }
+  if (epi == ifd::EPI_DDIM && c->use_noise && !noise) { set_error("ifd_ddim_step: use_noise requires noise"); return 2; }
+  if (epi == ifd::EPI_DDPM && !noise) { set_error("ifd_ddpm_step: noise required"); return 2; }
+  ifd::StepCoeffs sc;
+  std::memcpy(&sc, c, sizeof(sc));
+  return h->model->forward(img, gt, mask, 1, t, (int)B, H, W, epi, nullptr, &sc, img, gt, mask, noise, known,
+                           (hipStream_t)stream);
+}
+
+int ifd_ddim_step(ifd_handle* h, const int64_t* t, int64_t B, int H, int W, float* img, const float* gt,
+                  const float* mask, const float* noise, const float* known, const ifd_step_coeffs* c, void* stream) {
+  return step_common(h, ifd::EPI_DDIM, t, B, H, W, img, gt, mask, noise, known, c, stream);
+}
+
+int ifd_ddpm_step(ifd_handle* h, const int64_t* t, int64_t B, int H, int W, float* img, const float* gt,
+                  const float* mask, const float* noise, const float* known, const ifd_step_coeffs* c, void* stream) {
+  return step_common(h, ifd::EPI_DDPM, t, B, H, W, img, gt, mask, noise, known, c, stream);
+}
+
+static int update_common(int mode, const float* out6, int64_t B, int H, int W, float* img, const float* gt,
+                         const float* mask, const float* noise, const float* known, const ifd_step_coeffs* c,
+                         void* stream) {
+  if (!out6 || !img || !c) { set_error("ifd update: null argument"); return 2; }
+  if (c->inject && (!gt || !mask || !known)) { set_error("ifd update: inject requires gt, mask, known"); return 2; }
+  if ((mode == ifd::EPI_DDPM || c->use_noise) && !noise) { set_error("ifd update: noise required"); return 2; }
+  ifd::StepCoeffs sc;
+  std::memcpy(&sc, c, sizeof(sc));
+  ifd::launch_step(mode, sc, out6, img, gt, mask, noise, known, (int)B, H * W, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return 1; }
+  return 0;
+}
+
+int ifd_ddim_update(const float* out6, int64_t B, int H, int W, float* img, const float* gt, const float* mask,
+                    const float* noise, const float* known, const ifd_step_coeffs* c, void* stream) {
+  return update_common(ifd::EPI_DDIM, out6, B, H, W, img, gt, mask, noise, known, c, stream);
+}
+
+int ifd_ddpm_update(const float* out6, int64_t B, int H, int W, float* img, const float* gt, const float* mask,
+                    const float* noise, const float* known, const ifd_step_coeffs* c, void* stream) {
+  return update_common(ifd::EPI_DDPM, out6, B, H, W, img, gt, mask, noise, known, c, stream);
+}
+
+int ifd_blend(const float* result, const float* gt, const float* mask, int64_t B, int C, int H, int W, float* out,
+              void* stream) {
+  if (!result || !gt || !mask || !out) { set_error("ifd_blend: null argument"); return 2; }
+  ifd::launch_blend(result, gt, mask, out, (int)B, C, H * W, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return 1; }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,107 @@
+// Fused implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32), NHWC activations.
+//
+// One launch computes, for a 128-pixel x BN-channel output tile:
+//   out = conv3x3( act( xform( concat(in0, in1) ) ) ) [+ conv1x1(concat(s0, s1))] + bias [+ residual]
+// where
+//   act(v)   = silu(A[n,c] * v + B[n,c])   (GroupNorm-apply [+ scale/shift] + SiLU, fused prologue)
+//            | A[n,c] * v + B[n,c]         (GroupNorm-apply only: attention qkv)
+//            | v                           (no prologue)
+//   xform    = identity | nearest-up x2 | avg-pool 2x2   (ResBlock h_upd, code/nn.py:190-195)
+//   residual = identity | up x2 | down 2x2 of a raw tensor (ResBlock x_upd + identity skip, nn.py:212)
+// and zero padding is applied AFTER act, as torch pads the activated tensor (code/nn.py:153,176).
+// The 1x1 segment is the ResBlock skip_connection (code/nn.py:184) accumulated into the same
+// MFMA accumulators, so `skip(x) + h` costs no extra pass over HBM.
+#pragma once
+#include "common.h"
+
+namespace ifd {
+
+enum ConvAct : int { ACT_NONE = 0, ACT_AFFINE = 1, ACT_AFFINE_SILU = 2 };
+enum ConvXform : int { XF_NONE = 0, XF_UP = 1, XF_DOWN = 2 };
+enum ConvEpi : int { EPI_NHWC = 0, EPI_NCHW = 1, EPI_DDIM = 2, EPI_DDPM = 3 };
+
+// Per-step sampler coefficients, float64-derived on the host and rounded to fp32 once
+// (exactly what torch does when a float64 0-dim tensor multiplies an fp32 tensor).
+struct StepCoeffs {
+  // DDIM (code/test_inp_ddim_50.py:523-574)
+  float c_sqrt_1m_at;  // sqrt(1 - a_t)
+  float c_sqrt_at;     // sqrt(a_t)              (divisor)
+  float c_sqrt_ap;     // sqrt(a_prev)
+  float c_dir;         // sqrt(1 - a_prev - sigma^2)
+  float c_sigma;       // sigma
+  // DDPM (code/gaussian_diffusion.py:213-298 + test_inp_ddim_50.py:442-466)
+  float c_min_log, c_max_log, c_recip, c_recipm1, c_coef1, c_coef2, c_nonzero;
+  // injection (both): img*mask + (c_inj_a*gt + c_inj_b*known)*(1-mask)
+  float c_inj_a, c_inj_b;
+  int use_noise;  // DDIM: noise tensor present (tau > 0 and eta > 0)
+  int inject;     // tau > 0
+  int clip;       // clip_denoised
+  int pad;
+};
+
+struct ConvParams {
+  // primary input (concat of two NHWC sources along C)
+  const float* in0; int c0;
+  const float* in1; int c1;
+  int N, Hin, Win;   // input spatial size (before xform)
+  int H, W;          // conv / output spatial size
+  int act;           // ConvAct
+  const float* actA; const float* actB;  // [N, c0 + c1]
+  // weights
+  const float* wpack;  // [Cout_pad/BN][Cin_pad/8][TAPS][2][BN][4]
+  const float* bias;   // [Cout] (main + skip bias folded in)
+  int cin_pad, cout, cout_pad;
+  // 1x1 segment (ResBlock skip_connection), raw inputs at output resolution
+  const float* s0; int sc0;
+  const float* s1; int sc1;
+  const float* wskip;  // [Cout_pad/BN][Cs_pad/8][1][2][BN][4]
+  int cs_pad;
+  // residual (raw tensor with `cout` channels)
+  const float* res; int res_xform; int res_H, res_W;
+  // output
+  float* out;
+  int epi;
+  // tile geometry (host-computed)
+  int TW, TH, IMGS, tiles_x, tiles_y;
+  // sampler epilogue (EPI_DDIM / EPI_DDPM): all NCHW [N,3,H,W] except mask [N,1,H,W]
+  float* img; const float* gt; const float* mask; const float* noise; const float* known;
+  StepCoeffs sc;
+};
+
+// Launch with the tile configuration chosen from (cout, taps, xform). Returns hipError_t.
+int launch_conv(const ConvParams& p, int taps, int xform, int bn, hipStream_t stream);
+int conv_pick_bn(int cout, int taps, int H, int W, int N);
+
+// Shared elementwise step math, also used by the standalone step kernels (sampler.hip).
+__device__ __forceinline__ float ddim_step_value(const StepCoeffs& s, float img, float eps, float noise,
+                                                float gt, float mask, float known) {
+#pragma clang fp contract(off)
+  float x0 = (img - s.c_sqrt_1m_at * eps) / s.c_sqrt_at;
+  if (s.clip) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+  float dir = s.c_dir * eps;
+  float v = s.c_sqrt_ap * x0 + dir;
+  if (s.use_noise) v = v + s.c_sigma * noise;
+  if (s.inject) {
+    float keep = 1.0f - mask;
+    v = v * mask + (s.c_inj_a * gt + s.c_inj_b * known) * keep;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float ddpm_step_value(const StepCoeffs& s, float x, float eps, float var_v, float noise,
+                                                float gt, float mask, float known) {
+#pragma clang fp contract(off)
+  float frac = (var_v + 1.0f) / 2.0f;
+  float logvar = frac * s.c_max_log + (1.0f - frac) * s.c_min_log;
+  float x0 = s.c_recip * x - s.c_recipm1 * eps;
+  if (s.clip) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+  float mean = s.c_coef1 * x0 + s.c_coef2 * x;
+  float v = mean + (s.c_nonzero * expf(0.5f * logvar)) * noise;
+  if (s.inject) {
+    float keep = 1.0f - mask;
+    v = v * mask + (s.c_inj_a * gt + s.c_inj_b * known) * keep;
+  }
+  return v;
+}
+
+}  // namespace ifd

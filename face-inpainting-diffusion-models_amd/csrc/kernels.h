@@ -1,0 +1,22 @@
+// Host-side launchers of the non-conv kernels.
+#pragma once
+#include "conv.h"
+
+namespace ifd {
+
+int gn_slices(int HW, int* slice);
+int launch_gn(const float* p0, int c0, const float* p1, int c1, int N, int HW, const float* gamma, const float* beta,
+              const float* emb, int emb_stride, int emb_off, float* part, float* A, float* B, hipStream_t stream);
+void launch_pack_input(const float* x, const float* a, const float* m, int mode, int N, int HW, float* out,
+                       hipStream_t s);
+void launch_temb(const int64_t* t, const float* freqs, int mc, const float* w0t, const float* b0, const float* w2t,
+                 const float* b2, int E, int N, float* emb, hipStream_t s);
+void launch_emb_proj(const float* emb, int E, int N, const float* wt, const float* b, int J, float* out,
+                     hipStream_t s);
+void launch_attention(const float* qkv, int N, int T, int C, float scale, float* out, hipStream_t s);
+void launch_step(int mode, const StepCoeffs& sc, const float* out6, float* img, const float* gt, const float* mask,
+                 const float* noise, const float* known, int N, int HW, hipStream_t s);
+void launch_blend(const float* res, const float* gt, const float* mask, float* out, int N, int C, int HW,
+                  hipStream_t s);
+
+}  // namespace ifd

@@ -1,0 +1,256 @@
+// Small kernels around the conv core: input assembly, timestep embedding + MLP, the batched
+// ResBlock emb projections, QKV attention, and the standalone sampler step / blend kernels.
+#include "conv.h"
+#include "kernels.h"
+
+namespace ifd {
+
+// ---------------------------------------------------------------------------------------------
+// Input assembly (code/unet.py:197-200 + code/test_inp_ddim_50.py:373-385):
+//   [x(3), masked_image(3), mask, mask, mask] NCHW fp32  ->  NHWC with 16 channels (9 used, 7 zero)
+// mode 0: (x, masked_image, mask) given directly (model.forward)
+// mode 1: (img, gt, masks) from the sampler: masked = gt*keep + 0*(1-keep), mask_in = 1 - keep,
+//         keep = 1 - masks, bit-for-bit the fp32 ops of model_fn.
+__global__ void pack_input_kernel(const float* __restrict__ x, const float* __restrict__ a,
+                                  const float* __restrict__ m, int mode, int N, int HW, float* __restrict__ out) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * HW) return;
+  const int n = idx / HW, px = idx - n * HW;
+  const float* xn = x + (size_t)n * 3 * HW + px;
+  const float* an = a + (size_t)n * 3 * HW + px;
+  float mk = m[(size_t)n * HW + px];
+  f32x4 o0, o1, o2, o3;
+  o0[0] = xn[0]; o0[1] = xn[HW]; o0[2] = xn[2 * HW];
+  float m0, m1, m2;
+  if (mode == 0) {
+    m0 = an[0]; m1 = an[HW]; m2 = an[2 * HW];
+  } else {
+#pragma clang fp contract(off)
+    const float keep = 1.0f - mk;
+    const float zk = 0.0f * (1.0f - keep);
+    m0 = an[0] * keep + zk; m1 = an[HW] * keep + zk; m2 = an[2 * HW] * keep + zk;
+    mk = 1.0f - keep;
+  }
+  o0[3] = m0; o1[0] = m1; o1[1] = m2; o1[2] = mk; o1[3] = mk;
+  o2[0] = mk; o2[1] = 0.f; o2[2] = 0.f; o2[3] = 0.f;
+  o3[0] = 0.f; o3[1] = 0.f; o3[2] = 0.f; o3[3] = 0.f;
+  f32x4* dst = reinterpret_cast<f32x4*>(out + (size_t)idx * 16);
+  dst[0] = o0; dst[1] = o1; dst[2] = o2; dst[3] = o3;
+}
+
+void launch_pack_input(const float* x, const float* a, const float* m, int mode, int N, int HW, float* out,
+                       hipStream_t s) {
+  const int tot = N * HW;
+  hipLaunchKernelGGL(pack_input_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, x, a, m, mode, N, HW, out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// timestep_embedding (code/nn.py:51-61) + time_embed MLP (code/unet.py:44-48).
+// One block per image; weights pre-transposed to [in][out] so each thread's loads coalesce.
+__global__ __launch_bounds__(512) void temb_kernel(const int64_t* __restrict__ t, const float* __restrict__ freqs,
+                                                   int mc, const float* __restrict__ w0t, const float* __restrict__ b0,
+                                                   const float* __restrict__ w2t, const float* __restrict__ b2,
+                                                   int E, float* __restrict__ emb) {
+  extern __shared__ float sm[];
+  float* te = sm;        // [mc]
+  float* h1 = sm + mc;   // [E]
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float tf = (float)t[n];
+  const int half = mc / 2;
+  for (int i = tid; i < half; i += blockDim.x) {
+    const float arg = tf * freqs[i];
+    te[i] = cosf(arg);
+    te[half + i] = sinf(arg);
+  }
+  __syncthreads();
+  for (int j = tid; j < E; j += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < mc; ++k) acc += w0t[(size_t)k * E + j] * te[k];
+    h1[j] = silu_f(acc + b0[j]);
+  }
+  __syncthreads();
+  for (int j = tid; j < E; j += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < E; ++k) acc += w2t[(size_t)k * E + j] * h1[k];
+    emb[(size_t)n * E + j] = acc + b2[j];
+  }
+}
+
+void launch_temb(const int64_t* t, const float* freqs, int mc, const float* w0t, const float* b0, const float* w2t,
+                 const float* b2, int E, int N, float* emb, hipStream_t s) {
+  hipLaunchKernelGGL(temb_kernel, dim3(N), dim3(512), (mc + E) * sizeof(float), s, t, freqs, mc, w0t, b0, w2t, b2, E,
+                     emb);
+}
+
+// All 30 ResBlock emb projections of one eval in one launch (code/nn.py:167-170,199):
+//   Eall[n][j] = sum_k Wt[k][j] * silu(emb[n][k]) + b[j],   j over the concatenated [2*Cout] rows.
+constexpr int EP_NB = 16;
+__global__ __launch_bounds__(256) void emb_proj_kernel(const float* __restrict__ emb, int E, int N,
+                                                       const float* __restrict__ wt, const float* __restrict__ b,
+                                                       int J, float* __restrict__ out) {
+  extern __shared__ float se[];  // [EP_NB][E]
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int nb = 0; nb < N; nb += EP_NB) {
+    const int nn = min(EP_NB, N - nb);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nn * E; i += blockDim.x) se[i] = silu_f(emb[(size_t)nb * E + i]);
+    __syncthreads();
+    if (j < J) {
+      float acc[EP_NB];
+#pragma unroll
+      for (int q = 0; q < EP_NB; ++q) acc[q] = 0.f;
+      for (int k = 0; k < E; ++k) {
+        const float w = wt[(size_t)k * J + j];
+#pragma unroll
+        for (int q = 0; q < EP_NB; ++q) acc[q] += w * se[q * E + k];
+      }
+      const float bj = b[j];
+      for (int q = 0; q < nn; ++q) out[(size_t)(nb + q) * J + j] = acc[q] + bj;
+    }
+  }
+}
+
+void launch_emb_proj(const float* emb, int E, int N, const float* wt, const float* b, int J, float* out,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(emb_proj_kernel, dim3((J + 255) / 256), dim3(256), EP_NB * E * sizeof(float), s, emb, E, N, wt,
+                     b, J, out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// QKVAttention (code/nn.py:222-235), "chunk first" order: q = qkv[..., 0:C], k = [C:2C], v = [2C:3C],
+// head h = channels [64h, 64h+64) of each. w = softmax((q*s)(k*s)^T) in fp32, a = w v.
+// One block per (n, head, 32 queries); the whole score row (T <= 256) stays in LDS so the softmax
+// is the exact max-subtract / exp / multiply-by-reciprocal of the reference (no online rescale).
+constexpr int AT_QB = 32;
+constexpr int AT_CH = 64;
+constexpr int AT_KB = 64;
+
+__global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ qkv, int T, int C, float scale,
+                                                        float* __restrict__ out) {
+  __shared__ float Qs[AT_QB][AT_CH + 1];
+  __shared__ float KV[AT_KB][AT_CH + 1];
+  __shared__ float S[AT_QB][256 + 1];
+  const int tid = threadIdx.x;
+  const int qb = blockIdx.x, head = blockIdx.y, n = blockIdx.z;
+  const int t0 = qb * AT_QB;
+  const size_t rowstride = 3 * (size_t)C;
+  const float* base = qkv + (size_t)n * T * rowstride;
+  for (int i = tid; i < AT_QB * AT_CH; i += 256) {
+    const int r = i / AT_CH, c = i % AT_CH;
+    const int tq = t0 + r;
+    Qs[r][c] = tq < T ? base[(size_t)tq * rowstride + head * AT_CH + c] * scale : 0.f;
+  }
+  const int r = tid / 8, u = tid % 8;
+  for (int kt = 0; kt < T; kt += AT_KB) {
+    __syncthreads();
+    for (int i = tid; i < AT_KB * AT_CH; i += 256) {
+      const int s = i / AT_CH, c = i % AT_CH;
+      const int ts = kt + s;
+      KV[s][c] = ts < T ? base[(size_t)ts * rowstride + C + head * AT_CH + c] * scale : 0.f;
+    }
+    __syncthreads();
+    for (int jj = 0; jj < AT_KB / 8; ++jj) {
+      const int s = u + 8 * jj;
+      if (kt + s < T) {
+        float acc = 0.f;
+        for (int c = 0; c < AT_CH; ++c) acc += Qs[r][c] * KV[s][c];
+        S[r][kt + s] = acc;
+      }
+    }
+  }
+  __syncthreads();
+  // softmax: 4 waves x 8 rows, lanes stride over the row
+  {
+    const int wave = tid / 64, lane = tid % 64;
+    for (int rr = 0; rr < AT_QB / 4; ++rr) {
+      const int row = wave * (AT_QB / 4) + rr;
+      float mx = -INFINITY;
+      for (int s = lane; s < T; s += 64) mx = fmaxf(mx, S[row][s]);
+      for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+      float sum = 0.f;
+      for (int s = lane; s < T; s += 64) {
+        const float e = expf(S[row][s] - mx);
+        S[row][s] = e;
+        sum += e;
+      }
+      for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+      const float inv = 1.0f / sum;
+      for (int s = lane; s < T; s += 64) S[row][s] = S[row][s] * inv;
+    }
+  }
+  float acc[8];
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  for (int kt = 0; kt < T; kt += AT_KB) {
+    __syncthreads();
+    for (int i = tid; i < AT_KB * AT_CH; i += 256) {
+      const int s = i / AT_CH, c = i % AT_CH;
+      const int ts = kt + s;
+      KV[s][c] = ts < T ? base[(size_t)ts * rowstride + 2 * C + head * AT_CH + c] : 0.f;
+    }
+    __syncthreads();
+    const int smax = min(AT_KB, T - kt);
+    for (int s = 0; s < smax; ++s) {
+      const float pw = S[r][kt + s];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += pw * KV[s][u + 8 * q];
+    }
+  }
+  const int tq = t0 + r;
+  if (tq < T)
+    for (int q = 0; q < 8; ++q) out[((size_t)n * T + tq) * C + head * AT_CH + u + 8 * q] = acc[q];
+}
+
+void launch_attention(const float* qkv, int N, int T, int C, float scale, float* out, hipStream_t s) {
+  dim3 grid((T + AT_QB - 1) / AT_QB, C / AT_CH, N);
+  hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, T, C, scale, out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Standalone sampler updates on a model output [N,6,H,W] (same math as the fused conv epilogue).
+__global__ void step_kernel(int mode, const StepCoeffs sc, const float* __restrict__ out6, float* __restrict__ img,
+                            const float* __restrict__ gt, const float* __restrict__ mask,
+                            const float* __restrict__ noise, const float* __restrict__ known, int N, int HW) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * 3 * HW) return;
+  const int px = idx % HW, nc = idx / HW, c = nc % 3, n = nc / 3;
+  const float eps = out6[((size_t)n * 6 + c) * HW + px];
+  const size_t om = (size_t)n * HW + px;
+  const float mk = sc.inject ? mask[om] : 0.f;
+  const float g = sc.inject ? gt[idx] : 0.f;
+  const float kn = sc.inject ? known[idx] : 0.f;
+  float v;
+  if (mode == EPI_DDIM) {
+    v = ddim_step_value(sc, img[idx], eps, sc.use_noise ? noise[idx] : 0.f, g, mk, kn);
+  } else {
+    const float var_v = out6[((size_t)n * 6 + c + 3) * HW + px];
+    v = ddpm_step_value(sc, img[idx], eps, var_v, noise[idx], g, mk, kn);
+  }
+  img[idx] = v;
+}
+
+void launch_step(int mode, const StepCoeffs& sc, const float* out6, float* img, const float* gt, const float* mask,
+                 const float* noise, const float* known, int N, int HW, hipStream_t s) {
+  const int tot = N * 3 * HW;
+  hipLaunchKernelGGL(step_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, mode, sc, out6, img, gt, mask, noise,
+                     known, N, HW);
+}
+
+// final blend (code/test_inp_ddim_50.py:692-696): out = result*mask + gt*(1 - mask)
+__global__ void blend_kernel(const float* __restrict__ res, const float* __restrict__ gt,
+                             const float* __restrict__ mask, float* __restrict__ out, int N, int C, int HW) {
+#pragma clang fp contract(off)
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * C * HW) return;
+  const int px = idx % HW, n = idx / (C * HW);
+  const float m = mask[(size_t)n * HW + px];
+  const float keep = 1.0f - m;
+  out[idx] = res[idx] * m + gt[idx] * keep;
+}
+
+void launch_blend(const float* res, const float* gt, const float* mask, float* out, int N, int C, int HW,
+                  hipStream_t s) {
+  const int tot = N * C * HW;
+  hipLaunchKernelGGL(blend_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, res, gt, mask, out, N, C, HW);
+}
+
+}  // namespace ifd

@@ -1,0 +1,110 @@
+// 9-channel ADM UNet execution plan (code/unet.py:14-200) on the HIP kernels.
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/ifd.h"
+#include "kernels.h"
+
+namespace ifd {
+
+struct ConvW {
+  int cin = 0, cin_pad = 0, cout = 0, cout_pad = 0, bn = 0, taps = 9;
+  size_t w_off = 0, b_off = 0;     // float offsets in the device weight blob
+  int cs = 0, cs_pad = 0;          // 1x1 skip segment input channels
+  size_t ws_off = 0;
+  bool has_skip = false;
+  std::string wname, bname, swname, sbname;  // source parameter names
+};
+
+struct GNW {
+  size_t g_off = 0, b_off = 0;
+  int C = 0;
+  std::string prefix;
+};
+
+struct ResP {
+  std::string prefix;
+  int cin = 0, cout = 0, c_cat = 0;  // c_cat: channels of the concatenated skip tensor (output blocks)
+  int xf = XF_NONE;
+  GNW gn1, gn2;
+  ConvW conv1, conv2;
+  int emb_off = 0;
+};
+
+struct AttnP {
+  std::string prefix;
+  int C = 0;
+  GNW gn;
+  ConvW qkv, proj;
+};
+
+enum LayerKind { L_RES = 0, L_ATTN = 1 };
+struct LayerP {
+  int kind;
+  int idx;
+  int res_in;  // spatial size at input
+};
+
+struct ParamSpec {
+  std::string name;
+  std::vector<int64_t> shape;
+};
+
+class Model {
+ public:
+  explicit Model(const ifd_config& cfg);
+  ~Model();
+
+  const std::vector<ParamSpec>& params() const { return params_; }
+  int load(const std::string& name, const float* data, const int64_t* shape, int ndim);
+  int finalize();
+  int forward(const float* x, const float* a, const float* m, int pack_mode, const int64_t* t, int B, int H, int W,
+              int epi, float* out6, const StepCoeffs* sc, float* img, const float* gt, const float* mask,
+              const float* noise, const float* known, hipStream_t s);
+  int64_t weight_bytes() const { return (int64_t)wblob_floats_ * 4; }
+  int64_t workspace_bytes() const { return (int64_t)ws_floats_ * 4; }
+
+ private:
+  void build_plan();
+  void add_param(const std::string& n, std::vector<int64_t> shape);
+  int ensure_workspace(int B);
+  int run_res(const ResP& r, const float* in0, int c0, const float* in1, int c1, int N, int Hin, float* out,
+              hipStream_t s);
+  int run_attn(const AttnP& a, const float* in, int N, int Hin, float* out, hipStream_t s);
+  int run_conv(const ConvW& cw, const float* in0, int c0, const float* in1, int c1, int N, int Hin, int H, int xf,
+               int act, const float* A, const float* Bc, const float* s0, int sc0, const float* s1, int sc1,
+               const float* res, int res_xf, int resH, float* out, int epi, hipStream_t s,
+               const StepCoeffs* sc = nullptr, float* img = nullptr, const float* gt = nullptr,
+               const float* mask = nullptr, const float* noise = nullptr, const float* known = nullptr);
+
+  ifd_config cfg_;
+  std::vector<ParamSpec> params_;
+  std::map<std::string, std::vector<float>> host_;  // loaded parameters (host copies until finalize)
+
+  // plan
+  ConvW conv_in_, conv_out_;
+  GNW gn_out_;
+  std::vector<ResP> res_;
+  std::vector<AttnP> attn_;
+  std::vector<std::vector<LayerP>> in_blocks_, out_blocks_;
+  std::vector<LayerP> mid_;
+  std::vector<int> in_ch_, in_res_;  // channels / resolution of each input block's output
+  int emb_dim_ = 0, emb_total_ = 0;
+  size_t te_w0_ = 0, te_b0_ = 0, te_w2_ = 0, te_b2_ = 0, freqs_ = 0, embw_ = 0, embb_ = 0;
+
+  // device memory
+  float* wblob_ = nullptr;
+  size_t wblob_floats_ = 0;
+  bool finalized_ = false;
+  float* ws_ = nullptr;
+  size_t ws_floats_ = 0;
+  int ws_B_ = 0;
+  // workspace carve (float offsets), valid for ws_B_
+  size_t o_x0_ = 0, o_bufs_[3] = {0, 0, 0}, o_t1_ = 0, o_qkv_ = 0, o_ao_ = 0, o_A_ = 0, o_B_ = 0, o_part_ = 0,
+         o_emb_ = 0, o_E_ = 0;
+  std::vector<size_t> o_hs_;
+};
+
+}  // namespace ifd

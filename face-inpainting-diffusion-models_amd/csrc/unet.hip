@@ -1,0 +1,555 @@
+// UNet plan, weight packing and forward orchestration (host side of the HIP library).
+//
+// Plan mirrors UNetModel.__init__ (code/unet.py:43-152) with resblock_updown=True,
+// use_scale_shift_norm=True and the 9-channel first conv of DiffusionInpaintingModel
+// (code/unet.py:184-188). Activations are NHWC fp32 in one workspace arena; skip tensors of the
+// input blocks stay resident until the matching output block consumes them (no torch.cat: the
+// conv reads the two sources by channel range).
+#include "unet.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace ifd {
+
+static int ceil_to(int v, int m) { return (v + m - 1) / m * m; }
+
+Model::Model(const ifd_config& cfg) : cfg_(cfg) { build_plan(); }
+
+Model::~Model() {
+  if (wblob_) (void)hipFree(wblob_);
+  if (ws_) (void)hipFree(ws_);
+}
+
+void Model::add_param(const std::string& n, std::vector<int64_t> shape) { params_.push_back({n, std::move(shape)}); }
+
+static ConvW make_conv(const std::string& w, const std::string& b, int cin, int cout, int taps) {
+  ConvW c;
+  c.cin = cin;
+  c.cin_pad = ceil_to(cin, 8);
+  c.cout = cout;
+  c.bn = conv_pick_bn(cout, taps, 0, 0, 0);
+  c.cout_pad = ceil_to(cout, c.bn);
+  c.taps = taps;
+  c.wname = w;
+  c.bname = b;
+  return c;
+}
+
+void Model::build_plan() {
+  const int mc = cfg_.model_channels;
+  emb_dim_ = 4 * mc;
+  add_param("time_embed.0.weight", {emb_dim_, mc});
+  add_param("time_embed.0.bias", {emb_dim_});
+  add_param("time_embed.2.weight", {emb_dim_, emb_dim_});
+  add_param("time_embed.2.bias", {emb_dim_});
+
+  auto has_attn = [&](int ds) {
+    for (int i = 0; i < cfg_.num_attention; ++i)
+      if (cfg_.attention_ds[i] == ds) return true;
+    return false;
+  };
+  auto add_res = [&](const std::string& p, int cin, int cout, int xf, int c_cat) {
+    ResP r;
+    r.prefix = p;
+    r.cin = cin;
+    r.cout = cout;
+    r.xf = xf;
+    r.c_cat = c_cat;
+    r.gn1.C = cin;
+    r.gn1.prefix = p + "in_layers.0.";
+    r.conv1 = make_conv(p + "in_layers.2.weight", p + "in_layers.2.bias", cin, cout, 9);
+    r.gn2.C = cout;
+    r.gn2.prefix = p + "out_layers.0.";
+    r.conv2 = make_conv(p + "out_layers.3.weight", p + "out_layers.3.bias", cout, cout, 9);
+    add_param(p + "in_layers.0.weight", {cin});
+    add_param(p + "in_layers.0.bias", {cin});
+    add_param(p + "in_layers.2.weight", {cout, cin, 3, 3});
+    add_param(p + "in_layers.2.bias", {cout});
+    add_param(p + "emb_layers.1.weight", {2 * cout, emb_dim_});
+    add_param(p + "emb_layers.1.bias", {2 * cout});
+    add_param(p + "out_layers.0.weight", {cout});
+    add_param(p + "out_layers.0.bias", {cout});
+    add_param(p + "out_layers.3.weight", {cout, cout, 3, 3});
+    add_param(p + "out_layers.3.bias", {cout});
+    if (cin != cout) {
+      add_param(p + "skip_connection.weight", {cout, cin, 1, 1});
+      add_param(p + "skip_connection.bias", {cout});
+      r.conv2.has_skip = true;
+      r.conv2.cs = cin;
+      r.conv2.cs_pad = ceil_to(cin, 8);
+      r.conv2.swname = p + "skip_connection.weight";
+      r.conv2.sbname = p + "skip_connection.bias";
+    }
+    r.emb_off = emb_total_;
+    emb_total_ += 2 * cout;
+    res_.push_back(r);
+    return (int)res_.size() - 1;
+  };
+  auto add_attn = [&](const std::string& p, int c) {
+    AttnP a;
+    a.prefix = p;
+    a.C = c;
+    a.gn.C = c;
+    a.gn.prefix = p + "norm.";
+    a.qkv = make_conv(p + "qkv.weight", p + "qkv.bias", c, 3 * c, 1);
+    a.proj = make_conv(p + "proj_out.weight", p + "proj_out.bias", c, c, 1);
+    add_param(p + "norm.weight", {c});
+    add_param(p + "norm.bias", {c});
+    add_param(p + "qkv.weight", {3 * c, c, 1});
+    add_param(p + "qkv.bias", {3 * c});
+    add_param(p + "proj_out.weight", {c, c, 1});
+    add_param(p + "proj_out.bias", {c});
+    attn_.push_back(a);
+    return (int)attn_.size() - 1;
+  };
+
+  int res = cfg_.image_size;
+  int ch = cfg_.channel_mult[0] * mc;
+  conv_in_ = make_conv("input_blocks.0.0.weight", "input_blocks.0.0.bias", 16, ch, 9);
+  conv_in_.cin = cfg_.in_channels;  // packed input carries 16 channels, 9 real
+  conv_in_.cin_pad = 16;
+  add_param("input_blocks.0.0.weight", {ch, cfg_.in_channels, 3, 3});
+  add_param("input_blocks.0.0.bias", {ch});
+  in_blocks_.push_back({});
+  in_ch_.push_back(ch);
+  in_res_.push_back(res);
+  int ds = 1;
+  for (int level = 0; level < cfg_.num_levels; ++level) {
+    const int mult = cfg_.channel_mult[level];
+    for (int k = 0; k < cfg_.num_res_blocks; ++k) {
+      const int i = (int)in_blocks_.size();
+      const std::string p = "input_blocks." + std::to_string(i) + ".";
+      const int out = mult * mc;
+      std::vector<LayerP> L;
+      L.push_back({L_RES, add_res(p + "0.", ch, out, XF_NONE, 0), res});
+      ch = out;
+      if (has_attn(ds)) L.push_back({L_ATTN, add_attn(p + "1.", ch), res});
+      in_blocks_.push_back(L);
+      in_ch_.push_back(ch);
+      in_res_.push_back(res);
+    }
+    if (level != cfg_.num_levels - 1) {
+      const int i = (int)in_blocks_.size();
+      const std::string p = "input_blocks." + std::to_string(i) + ".";
+      std::vector<LayerP> L;
+      L.push_back({L_RES, add_res(p + "0.", ch, ch, XF_DOWN, 0), res});
+      in_blocks_.push_back(L);
+      ds *= 2;
+      res /= 2;
+      in_ch_.push_back(ch);
+      in_res_.push_back(res);
+    }
+  }
+  mid_.push_back({L_RES, add_res("middle_block.0.", ch, ch, XF_NONE, 0), res});
+  mid_.push_back({L_ATTN, add_attn("middle_block.1.", ch), res});
+  mid_.push_back({L_RES, add_res("middle_block.2.", ch, ch, XF_NONE, 0), res});
+  std::vector<int> chans = in_ch_;
+  int j = 0;
+  for (int level = cfg_.num_levels - 1; level >= 0; --level) {
+    const int mult = cfg_.channel_mult[level];
+    for (int k = 0; k < cfg_.num_res_blocks + 1; ++k) {
+      const int ich = chans.back();
+      chans.pop_back();
+      const std::string p = "output_blocks." + std::to_string(j) + ".";
+      const int out = mc * mult;
+      std::vector<LayerP> L;
+      L.push_back({L_RES, add_res(p + "0.", ch + ich, out, XF_NONE, ich), res});
+      ch = out;
+      if (has_attn(ds)) L.push_back({L_ATTN, add_attn(p + "1.", ch), res});
+      if (level && k == cfg_.num_res_blocks) {
+        L.push_back({L_RES, add_res(p + std::to_string(L.size()) + ".", ch, ch, XF_UP, 0), res});
+        ds /= 2;
+        res *= 2;
+      }
+      out_blocks_.push_back(L);
+      ++j;
+    }
+  }
+  gn_out_.C = ch;
+  gn_out_.prefix = "out.0.";
+  add_param("out.0.weight", {ch});
+  add_param("out.0.bias", {ch});
+  conv_out_ = make_conv("out.2.weight", "out.2.bias", ch, cfg_.out_channels, 9);
+  add_param("out.2.weight", {cfg_.out_channels, ch, 3, 3});
+  add_param("out.2.bias", {cfg_.out_channels});
+}
+
+int Model::load(const std::string& name_in, const float* data, const int64_t* shape, int ndim) {
+  std::string name = name_in;
+  if (name.rfind("base_model.", 0) == 0) name = name.substr(11);
+  const ParamSpec* spec = nullptr;
+  for (auto& p : params_)
+    if (p.name == name) spec = &p;
+  IFD_REQUIRE(spec != nullptr, "unexpected parameter " + name_in);
+  IFD_REQUIRE((int)spec->shape.size() == ndim, "rank mismatch for " + name);
+  size_t numel = 1;
+  for (int i = 0; i < ndim; ++i) {
+    IFD_REQUIRE(spec->shape[i] == shape[i], "shape mismatch for " + name);
+    numel *= (size_t)shape[i];
+  }
+  std::vector<float> buf(numel);
+  IFD_CHECK_HIP(hipMemcpy(buf.data(), data, numel * sizeof(float), hipMemcpyDefault));
+  host_[name] = std::move(buf);
+  finalized_ = false;
+  return 0;
+}
+
+// Packed conv weight layout: [Cout_pad/BN][Cin_pad/8][taps][q=2][BN][4], element
+//   W[ct*BN + col][ch*8 + q*4 + j][tap/3][tap%3]  (zero outside [Cout) x [Cin)).
+static void pack_conv(const std::vector<float>& w, int cout, int cin, int taps, int bn, int cin_pad, int cout_pad,
+                      std::vector<float>& blob, size_t off) {
+  const int nch = cin_pad / 8;
+  for (int ct = 0; ct < cout_pad / bn; ++ct)
+    for (int chk = 0; chk < nch; ++chk)
+      for (int tap = 0; tap < taps; ++tap)
+        for (int q = 0; q < 2; ++q)
+          for (int col = 0; col < bn; ++col)
+            for (int jj = 0; jj < 4; ++jj) {
+              const int co = ct * bn + col, ci = chk * 8 + q * 4 + jj;
+              float v = 0.f;
+              if (co < cout && ci < cin) v = w[((size_t)co * cin + ci) * taps + tap];
+              blob[off + ((((size_t)(ct * nch + chk) * taps + tap) * 2 + q) * bn + col) * 4 + jj] = v;
+            }
+}
+
+int Model::finalize() {
+  for (auto& p : params_) IFD_REQUIRE(host_.count(p.name), "missing parameter " + p.name);
+  // size the blob
+  size_t n = 0;
+  auto reserve = [&](size_t cnt) {
+    size_t o = n;
+    n += (cnt + 3) / 4 * 4;  // keep 16-byte alignment
+    return o;
+  };
+  auto plan_conv = [&](ConvW& c) {
+    c.w_off = reserve((size_t)c.cout_pad * c.cin_pad * c.taps);
+    c.b_off = reserve(c.cout_pad);
+    if (c.has_skip) c.ws_off = reserve((size_t)c.cout_pad * c.cs_pad);
+  };
+  auto plan_gn = [&](GNW& g) {
+    g.g_off = reserve(g.C);
+    g.b_off = reserve(g.C);
+  };
+  const int mc = cfg_.model_channels;
+  te_w0_ = reserve((size_t)mc * emb_dim_);
+  te_b0_ = reserve(emb_dim_);
+  te_w2_ = reserve((size_t)emb_dim_ * emb_dim_);
+  te_b2_ = reserve(emb_dim_);
+  freqs_ = reserve(mc / 2);
+  embw_ = reserve((size_t)emb_dim_ * emb_total_);
+  embb_ = reserve(emb_total_);
+  plan_conv(conv_in_);
+  for (auto& r : res_) {
+    plan_gn(r.gn1);
+    plan_conv(r.conv1);
+    plan_gn(r.gn2);
+    plan_conv(r.conv2);
+  }
+  for (auto& a : attn_) {
+    plan_gn(a.gn);
+    plan_conv(a.qkv);
+    plan_conv(a.proj);
+  }
+  plan_gn(gn_out_);
+  plan_conv(conv_out_);
+
+  std::vector<float> blob(n, 0.f);
+  auto put = [&](size_t off, const std::vector<float>& v) { std::copy(v.begin(), v.end(), blob.begin() + off); };
+  auto fill_conv = [&](ConvW& c) {
+    pack_conv(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob, c.w_off);
+    const auto& b = host_[c.bname];
+    for (int i = 0; i < c.cout; ++i) blob[c.b_off + i] = b[i];
+    if (c.has_skip) {
+      pack_conv(host_[c.swname], c.cout, c.cs, 1, c.bn, c.cs_pad, c.cout_pad, blob, c.ws_off);
+      const auto& sb = host_[c.sbname];
+      // bias of h (conv) and of skip_connection(x) are both added once per output element
+      for (int i = 0; i < c.cout; ++i) blob[c.b_off + i] = b[i] + sb[i];
+    }
+  };
+  auto fill_gn = [&](GNW& g) {
+    put(g.g_off, host_[g.prefix + "weight"]);
+    put(g.b_off, host_[g.prefix + "bias"]);
+  };
+  // time embedding: transpose [out][in] -> [in][out]
+  {
+    const auto& w0 = host_["time_embed.0.weight"];
+    for (int o = 0; o < emb_dim_; ++o)
+      for (int i = 0; i < mc; ++i) blob[te_w0_ + (size_t)i * emb_dim_ + o] = w0[(size_t)o * mc + i];
+    put(te_b0_, host_["time_embed.0.bias"]);
+    const auto& w2 = host_["time_embed.2.weight"];
+    for (int o = 0; o < emb_dim_; ++o)
+      for (int i = 0; i < emb_dim_; ++i) blob[te_w2_ + (size_t)i * emb_dim_ + o] = w2[(size_t)o * emb_dim_ + i];
+    put(te_b2_, host_["time_embed.2.bias"]);
+    // freqs = exp(-ln(10000) * arange(half, fp32) / half) in fp32, as code/nn.py:54-56
+    const int half = mc / 2;
+    const float c = (float)(-std::log(10000.0));
+    for (int i = 0; i < half; ++i) {
+      volatile float prod = c * (float)i;
+      volatile float q = prod / (float)half;
+      blob[freqs_ + i] = std::exp(q);
+    }
+  }
+  for (auto& r : res_) {
+    const auto& w = host_[r.prefix + "emb_layers.1.weight"];
+    const auto& b = host_[r.prefix + "emb_layers.1.bias"];
+    for (int o = 0; o < 2 * r.cout; ++o) {
+      for (int i = 0; i < emb_dim_; ++i)
+        blob[embw_ + (size_t)i * emb_total_ + r.emb_off + o] = w[(size_t)o * emb_dim_ + i];
+      blob[embb_ + r.emb_off + o] = b[o];
+    }
+  }
+  fill_conv(conv_in_);
+  for (auto& r : res_) {
+    fill_gn(r.gn1);
+    fill_conv(r.conv1);
+    fill_gn(r.gn2);
+    fill_conv(r.conv2);
+  }
+  for (auto& a : attn_) {
+    fill_gn(a.gn);
+    fill_conv(a.qkv);
+    fill_conv(a.proj);
+  }
+  fill_gn(gn_out_);
+  fill_conv(conv_out_);
+
+  if (wblob_) IFD_CHECK_HIP(hipFree(wblob_));
+  wblob_ = nullptr;
+  IFD_CHECK_HIP(hipMalloc(&wblob_, n * sizeof(float)));
+  IFD_CHECK_HIP(hipMemcpy(wblob_, blob.data(), n * sizeof(float), hipMemcpyHostToDevice));
+  wblob_floats_ = n;
+  finalized_ = true;
+  return 0;
+}
+
+int Model::ensure_workspace(int B) {
+  if (ws_ && B <= ws_B_) return 0;
+  const int R = cfg_.image_size;
+  size_t n = 0;
+  auto reserve = [&](size_t cnt) {
+    size_t o = n;
+    n += (cnt + 63) / 64 * 64;
+    return o;
+  };
+  size_t maxact = 0, maxqkv = 1, maxC = 16;
+  o_hs_.clear();
+  for (size_t i = 0; i < in_ch_.size(); ++i) {
+    const size_t sz = (size_t)B * in_res_[i] * in_res_[i] * in_ch_[i];
+    o_hs_.push_back(reserve(sz));
+    maxact = std::max(maxact, sz);
+  }
+  for (auto& r : res_) {
+    maxC = std::max<size_t>(maxC, std::max(r.cin, r.cout));
+  }
+  // worst activation size over all layers: every layer output is B * res^2 * C with res <= R
+  for (auto& blk : out_blocks_)
+    for (auto& L : blk) {
+      int C = L.kind == L_RES ? res_[L.idx].cout : attn_[L.idx].C;
+      int rr = L.res_in * ((L.kind == L_RES && res_[L.idx].xf == XF_UP) ? 2 : 1);
+      maxact = std::max(maxact, (size_t)B * rr * rr * C);
+    }
+  for (auto& L : mid_) {
+    int C = L.kind == L_RES ? res_[L.idx].cout : attn_[L.idx].C;
+    maxact = std::max(maxact, (size_t)B * L.res_in * L.res_in * C);
+  }
+  for (auto& a : attn_) (void)a;
+  for (size_t i = 0; i < in_blocks_.size(); ++i)
+    for (auto& L : in_blocks_[i])
+      if (L.kind == L_ATTN) maxqkv = std::max(maxqkv, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C * 3);
+  for (auto& blk : out_blocks_)
+    for (auto& L : blk)
+      if (L.kind == L_ATTN) maxqkv = std::max(maxqkv, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C * 3);
+  for (auto& L : mid_)
+    if (L.kind == L_ATTN) maxqkv = std::max(maxqkv, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C * 3);
+  o_x0_ = reserve((size_t)B * R * R * 16);
+  for (int k = 0; k < 3; ++k) o_bufs_[k] = reserve(maxact);
+  o_t1_ = reserve(maxact);
+  o_qkv_ = reserve(maxqkv);
+  o_ao_ = reserve(maxqkv / 3 + 1);
+  o_A_ = reserve((size_t)B * maxC);
+  o_B_ = reserve((size_t)B * maxC);
+  int slice;
+  const int nsl = gn_slices(R * R, &slice);
+  o_part_ = reserve((size_t)B * nsl * 32 * 3);
+  o_emb_ = reserve((size_t)B * emb_dim_);
+  o_E_ = reserve((size_t)B * emb_total_);
+  if (ws_) IFD_CHECK_HIP(hipFree(ws_));
+  ws_ = nullptr;
+  IFD_CHECK_HIP(hipMalloc(&ws_, n * sizeof(float)));
+  ws_floats_ = n;
+  ws_B_ = B;
+  return 0;
+}
+
+int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1, int c1, int N, int Hin, int H,
+                    int xf, int act, const float* A, const float* Bc, const float* s0, int sc0, const float* s1,
+                    int sc1, const float* res, int res_xf, int resH, float* out, int epi, hipStream_t s,
+                    const StepCoeffs* sc, float* img, const float* gt, const float* mask, const float* noise,
+                    const float* known) {
+  ConvParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.in0 = in0; p.c0 = c0; p.in1 = in1; p.c1 = c1;
+  p.N = N; p.Hin = Hin; p.Win = Hin; p.H = H; p.W = H;
+  p.act = act; p.actA = A; p.actB = Bc;
+  p.wpack = wblob_ + cw.w_off;
+  p.bias = wblob_ + cw.b_off;
+  p.cin_pad = cw.cin_pad; p.cout = cw.cout; p.cout_pad = cw.cout_pad;
+  if (cw.has_skip) {
+    p.s0 = s0; p.sc0 = sc0; p.s1 = s1; p.sc1 = sc1;
+    p.wskip = wblob_ + cw.ws_off;
+    p.cs_pad = cw.cs_pad;
+  }
+  p.res = res; p.res_xform = res_xf; p.res_H = resH; p.res_W = resH;
+  p.out = out;
+  p.epi = epi;
+  p.TW = std::min(H, 32);
+  p.TH = std::min(H, 128 / p.TW);
+  p.IMGS = 128 / (p.TH * p.TW);
+  p.tiles_x = H / p.TW;
+  p.tiles_y = H / p.TH;
+  if (sc) p.sc = *sc;
+  p.img = img; p.gt = gt; p.mask = mask; p.noise = noise; p.known = known;
+  IFD_REQUIRE(c0 % 8 == 0 && c1 % 8 == 0 && c0 + c1 == cw.cin_pad, "conv input channels");
+  IFD_REQUIRE(!cw.has_skip || (sc0 + sc1 == cw.cs_pad && sc0 % 8 == 0 && sc1 % 8 == 0), "skip channels");
+  int e = launch_conv(p, cw.taps, xf, cw.bn, s);
+  if (e) {
+    set_error(std::string("conv launch failed: ") + hipGetErrorString((hipError_t)e));
+    return 1;
+  }
+  return 0;
+}
+
+int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, int c1, int N, int Hin, float* out,
+                   hipStream_t s) {
+  float* A = ws_ + o_A_;
+  float* Bc = ws_ + o_B_;
+  float* part = ws_ + o_part_;
+  float* t1 = ws_ + o_t1_;
+  const int H = r.xf == XF_UP ? 2 * Hin : (r.xf == XF_DOWN ? Hin / 2 : Hin);
+  int e = launch_gn(in0, c0, in1, c1, N, Hin * Hin, wblob_ + r.gn1.g_off, wblob_ + r.gn1.b_off, nullptr, 0, 0, part, A,
+                    Bc, s);
+  IFD_REQUIRE(e == 0, "gn launch");
+  if (run_conv(r.conv1, in0, c0, in1, c1, N, Hin, H, r.xf, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
+               0, t1, EPI_NHWC, s))
+    return 1;
+  e = launch_gn(t1, r.cout, nullptr, 0, N, H * H, wblob_ + r.gn2.g_off, wblob_ + r.gn2.b_off, ws_ + o_E_, emb_total_,
+                r.emb_off, part, A, Bc, s);
+  IFD_REQUIRE(e == 0, "gn launch");
+  const float* res = r.conv2.has_skip ? nullptr : in0;
+  return run_conv(r.conv2, t1, r.cout, nullptr, 0, N, H, H, XF_NONE, ACT_AFFINE_SILU, A, Bc, in0, c0, in1, c1, res,
+                  r.xf, Hin, out, EPI_NHWC, s);
+}
+
+int Model::run_attn(const AttnP& a, const float* in, int N, int Hin, float* out, hipStream_t s) {
+  float* A = ws_ + o_A_;
+  float* Bc = ws_ + o_B_;
+  float* qkv = ws_ + o_qkv_;
+  float* ao = ws_ + o_ao_;
+  const int T = Hin * Hin;
+  int e = launch_gn(in, a.C, nullptr, 0, N, T, wblob_ + a.gn.g_off, wblob_ + a.gn.b_off, nullptr, 0, 0,
+                    ws_ + o_part_, A, Bc, s);
+  IFD_REQUIRE(e == 0, "gn launch");
+  if (run_conv(a.qkv, in, a.C, nullptr, 0, N, Hin, Hin, XF_NONE, ACT_AFFINE, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
+               0, qkv, EPI_NHWC, s))
+    return 1;
+  const float scale = (float)(1.0 / std::sqrt(std::sqrt((double)cfg_.num_head_channels)));
+  IFD_REQUIRE(cfg_.num_head_channels == 64, "attention kernel is specialised for 64-channel heads");
+  launch_attention(qkv, N, T, a.C, scale, ao, s);
+  return run_conv(a.proj, ao, a.C, nullptr, 0, N, Hin, Hin, XF_NONE, ACT_NONE, nullptr, nullptr, nullptr, 0, nullptr,
+                  0, in, XF_NONE, Hin, out, EPI_NHWC, s);
+}
+
+int Model::forward(const float* x, const float* a, const float* m, int pack_mode, const int64_t* t, int B, int H,
+                   int W, int epi, float* out6, const StepCoeffs* sc, float* img, const float* gt, const float* mask,
+                   const float* noise, const float* known, hipStream_t s) {
+  IFD_REQUIRE(H == cfg_.image_size && W == cfg_.image_size, "input size must equal image_size");
+  IFD_REQUIRE(B >= 1, "batch must be >= 1");
+  if (!finalized_) {
+    if (finalize()) return 1;
+  }
+  if (ensure_workspace(B)) return 1;
+  const int R = cfg_.image_size;
+  const int mc = cfg_.model_channels;
+  float* x0 = ws_ + o_x0_;
+  launch_pack_input(x, a, m, pack_mode, B, R * R, x0, s);
+  launch_temb(t, wblob_ + freqs_, mc, wblob_ + te_w0_, wblob_ + te_b0_, wblob_ + te_w2_, wblob_ + te_b2_, emb_dim_, B,
+              ws_ + o_emb_, s);
+  launch_emb_proj(ws_ + o_emb_, emb_dim_, B, wblob_ + embw_, wblob_ + embb_, emb_total_, ws_ + o_E_, s);
+
+  // input blocks
+  if (run_conv(conv_in_, x0, 16, nullptr, 0, B, R, R, XF_NONE, ACT_NONE, nullptr, nullptr, nullptr, 0, nullptr, 0,
+               nullptr, 0, 0, ws_ + o_hs_[0], EPI_NHWC, s))
+    return 1;
+  const float* cur = ws_ + o_hs_[0];
+  int cur_c = in_ch_[0], cur_r = in_res_[0];
+  for (size_t i = 1; i < in_blocks_.size(); ++i) {
+    const auto& L = in_blocks_[i];
+    for (size_t k = 0; k < L.size(); ++k) {
+      float* dst = (k + 1 == L.size()) ? ws_ + o_hs_[i] : ws_ + o_bufs_[k % 2];
+      if (L[k].kind == L_RES) {
+        const ResP& r = res_[L[k].idx];
+        if (run_res(r, cur, cur_c, nullptr, 0, B, cur_r, dst, s)) return 1;
+        cur_c = r.cout;
+        if (r.xf == XF_DOWN) cur_r /= 2;
+      } else {
+        if (run_attn(attn_[L[k].idx], cur, B, cur_r, dst, s)) return 1;
+      }
+      cur = dst;
+    }
+  }
+  // middle + output blocks: rotate three buffers, never writing the one being read
+  int bi = 0;
+  auto next_buf = [&](const float* avoid) {
+    for (int k = 0; k < 3; ++k) {
+      float* b = ws_ + o_bufs_[(bi + k) % 3];
+      if (b != avoid) {
+        bi = (bi + k + 1) % 3;
+        return b;
+      }
+    }
+    return (float*)nullptr;
+  };
+  for (auto& L : mid_) {
+    float* dst = next_buf(cur);
+    if (L.kind == L_RES) {
+      if (run_res(res_[L.idx], cur, cur_c, nullptr, 0, B, cur_r, dst, s)) return 1;
+    } else {
+      if (run_attn(attn_[L.idx], cur, B, cur_r, dst, s)) return 1;
+    }
+    cur = dst;
+  }
+  int hs_i = (int)in_blocks_.size() - 1;
+  for (auto& blk : out_blocks_) {
+    for (size_t k = 0; k < blk.size(); ++k) {
+      const LayerP& L = blk[k];
+      float* dst = next_buf(cur);
+      if (L.kind == L_RES) {
+        const ResP& r = res_[L.idx];
+        if (k == 0) {
+          const float* skip = ws_ + o_hs_[hs_i];
+          if (run_res(r, cur, cur_c, skip, in_ch_[hs_i], B, cur_r, dst, s)) return 1;
+          --hs_i;
+        } else {
+          if (run_res(r, cur, cur_c, nullptr, 0, B, cur_r, dst, s)) return 1;
+        }
+        cur_c = r.cout;
+        if (r.xf == XF_UP) cur_r *= 2;
+      } else {
+        if (run_attn(attn_[L.idx], cur, B, cur_r, dst, s)) return 1;
+      }
+      cur = dst;
+    }
+  }
+  // out: GN -> SiLU -> conv 3x3 -> [B,6,H,W] (or the fused sampler update)
+  float* A = ws_ + o_A_;
+  float* Bc = ws_ + o_B_;
+  int e = launch_gn(cur, cur_c, nullptr, 0, B, R * R, wblob_ + gn_out_.g_off, wblob_ + gn_out_.b_off, nullptr, 0, 0,
+                    ws_ + o_part_, A, Bc, s);
+  IFD_REQUIRE(e == 0, "gn launch");
+  return run_conv(conv_out_, cur, cur_c, nullptr, 0, B, R, R, XF_NONE, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0,
+                  nullptr, 0, 0, out6, epi, s, sc, img, gt, mask, noise, known);
+}
+
+}  // namespace ifd

@@ -1,0 +1,161 @@
+"""`DiffusionInpaintingModel` drop-in whose forward runs on the HIP library.
+
+Mirrors the Python surface the reference's sampling scripts use (code/unet.py:176-200,
+code/test_inp_ddim_50.py:325-385): parameters under the reference's `base_model.` state-dict keys,
+`load_state_dict(sd, strict=False) -> (missing, unexpected)`, `eval()`, `parameters()` (the
+scripts read `next(model.parameters()).device`), and `forward(x, t, masked_image=, mask=)`
+returning the [B, 6, H, W] fp32 output (eps + learned-range variance values).
+
+The parameters live as ordinary device tensors; on the first forward after a (re)load they are
+handed to the library (`ifd_load_weights`), which packs its own NHWC/KRSC-style copies.
+There is no CPU/PyTorch fallback: a CPU tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .topology import FULL, UNetConfig, state_dict_spec
+
+
+class _Node(torch.nn.Module):
+    pass
+
+
+def _config_struct(cfg: UNetConfig):
+    c = _lib.IfdConfig()
+    c.image_size = cfg.image_size
+    c.in_channels = cfg.in_channels
+    c.model_channels = cfg.model_channels
+    c.out_channels = cfg.out_channels
+    c.num_res_blocks = cfg.num_res_blocks
+    c.num_levels = len(cfg.channel_mult)
+    for i, m in enumerate(cfg.channel_mult):
+        c.channel_mult[i] = m
+    c.num_attention = len(cfg.attention_resolutions)
+    for i, d in enumerate(cfg.attention_resolutions):
+        c.attention_ds[i] = d
+    c.num_head_channels = cfg.num_head_channels
+    return c
+
+
+class Handle:
+    """Owns one `ifd_handle` (one per device)."""
+
+    def __init__(self, cfg: UNetConfig):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(L.ifd_create(ctypes.byref(_config_struct(cfg)), ctypes.byref(h)))
+        self.h = h
+        self.cfg = cfg
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) is not None and _lib._lib is not None:
+                _lib._lib.ifd_destroy(self.h)
+        except Exception:
+            pass
+
+    def param_names(self):
+        L = _lib.lib()
+        n = ctypes.c_int()
+        _lib.check(L.ifd_num_params(self.h, ctypes.byref(n)))
+        out = []
+        for i in range(n.value):
+            name = ctypes.c_char_p()
+            shape = (ctypes.c_int64 * 4)()
+            nd = ctypes.c_int()
+            _lib.check(L.ifd_param_info(self.h, i, ctypes.byref(name), shape, ctypes.byref(nd)))
+            out.append((name.value.decode(), tuple(shape[k] for k in range(nd.value))))
+        return out
+
+
+class DiffusionInpaintingModel(torch.nn.Module):
+    """9-channel inpainting UNet (code/unet.py:176-200) executed by libifd."""
+
+    def __init__(self, cfg: UNetConfig = FULL, device=None):
+        super().__init__()
+        self.cfg = cfg
+        self.base_model = _Node()
+        for key, shape in state_dict_spec(cfg, prefix=""):
+            node = self.base_model
+            parts = key.split(".")
+            for p in parts[:-1]:
+                if not hasattr(node, p) or not isinstance(getattr(node, p), torch.nn.Module):
+                    node.add_module(p, _Node())
+                node = getattr(node, p)
+            node.register_parameter(parts[-1], torch.nn.Parameter(torch.zeros(shape, device=device),
+                                                                  requires_grad=False))
+        self._handle = None
+        self._handle_device = None
+        self._dirty = True
+        self.dtype = torch.float32
+
+    # -- weights -------------------------------------------------------------------------------
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        res = super().load_state_dict(state_dict, strict=strict)
+        self._dirty = True
+        return res
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._dirty = True
+        return out
+
+    def handle(self, device):
+        if self._handle is None or self._handle_device != device:
+            with torch.cuda.device(device):
+                self._handle = Handle(self.cfg)
+            self._handle_device = device
+            self._dirty = True
+        if self._dirty:
+            L = _lib.lib()
+            torch.cuda.synchronize(device)
+            with torch.cuda.device(device):
+                for name, p in self.base_model.named_parameters():
+                    t = p.detach().to(device=device, dtype=torch.float32).contiguous()
+                    shape = (ctypes.c_int64 * max(1, t.dim()))(*t.shape)
+                    _lib.check(L.ifd_load_weights(self._handle.h, name.encode(), _lib.ptr(t), shape, t.dim()))
+                    del t
+                _lib.check(L.ifd_finalize(self._handle.h))
+            self._dirty = False
+        return self._handle
+
+    # -- forward -------------------------------------------------------------------------------
+    @staticmethod
+    def _dev_f32(t, device, name):
+        if not isinstance(t, torch.Tensor) or t.device != device:
+            raise RuntimeError(f"ifd: `{name}` must be a tensor on {device} (no CPU fallback)")
+        return t.to(torch.float32).contiguous()
+
+    def forward(self, x, t, masked_image=None, mask=None, **kwargs):
+        if masked_image is None or mask is None:
+            raise ValueError("DiffusionInpaintingModel.forward requires masked_image and mask")
+        if not x.is_cuda:
+            raise RuntimeError("ifd: the HIP UNet runs on GPU tensors only (no CPU fallback)")
+        dev = x.device
+        B, C, H, W = x.shape
+        assert C == 3 and masked_image.shape == (B, 3, H, W) and mask.shape == (B, 1, H, W), "shape mismatch"
+        xx = self._dev_f32(x, dev, "x")
+        mi = self._dev_f32(masked_image, dev, "masked_image")
+        mk = self._dev_f32(mask, dev, "mask")
+        tt = torch.as_tensor(t, device=dev).to(torch.int64).reshape(-1).expand(B).contiguous()
+        out = torch.empty(B, self.cfg.out_channels, H, W, device=dev, dtype=torch.float32)
+        h = self.handle(dev)
+        L = _lib.lib()
+        _lib.check(L.ifd_unet_forward(h.h, _lib.ptr(xx), _lib.ptr(mi), _lib.ptr(mk), _lib.ptr(tt), B, H, W,
+                                      _lib.ptr(out), _lib.stream_ptr(dev)))
+        return out
+
+    def memory(self):
+        h = self._handle
+        if h is None:
+            return 0, 0
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(_lib.lib().ifd_memory(h.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+
+UNetModelHIP = DiffusionInpaintingModel

@@ -1,0 +1,101 @@
+/* ifd — MI355X-native masked-inpainting diffusion sampler: the drop-in C ABI.
+ *
+ * Plain C, plain pointers and sizes; no torch types. All tensor arguments are DEVICE pointers
+ * to contiguous fp32 (int64 for timesteps) memory on the handle's device; every launch is
+ * asynchronous on `stream` (a hipStream_t passed as void*, e.g. torch's current stream).
+ * Status: 0 = ok, non-zero = error; the message is in ifd_last_error() (thread-local).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo):
+ *   ifd_create / ifd_param_* / ifd_load_weights / ifd_finalize
+ *       create_model_and_diffusion (code/train_inpainting.py:199-262): UNetModel(...) +
+ *       DiffusionInpaintingModel(base, 9) (code/unet.py:176-195) + load_state_dict(strict=False)
+ *       (code/train_inpainting.py:241; code/test_inp_ddim_50.py:349). Names are the reference's
+ *       state_dict keys, with or without the "base_model." prefix.
+ *   ifd_unet_forward
+ *       DiffusionInpaintingModel.forward(x, t, masked_image, mask) (code/unet.py:197-200)
+ *       -> UNetModel.forward (code/unet.py:154-173); NCHW in, NCHW [B,6,H,W] out.
+ *   ifd_ddim_step
+ *       one iteration of InpaintingSampler.inpainting_ddim_sample_loop
+ *       (code/test_inp_ddim_50.py:501-574): model_fn (:373-385) + UNet + the DDIM update and the
+ *       known-region re-injection, fused into the last conv's epilogue; updates img in place.
+ *   ifd_ddpm_step
+ *       one iteration of inpainting_p_sample_loop (code/test_inp_ddim_50.py:424-466) with
+ *       p_mean_variance (code/gaussian_diffusion.py:213-298), fused likewise.
+ *   ifd_ddim_update / ifd_ddpm_update
+ *       the same update math applied to an already computed model output [B,6,H,W].
+ *   ifd_blend
+ *       final blend result*mask + gt*(1-mask) (code/test_inp_ddim_50.py:692-696).
+ */
+#ifndef IFD_H
+#define IFD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ifd_config {
+  int image_size;          /* 256 */
+  int in_channels;         /* 9 (x, masked_image, mask x3) */
+  int model_channels;      /* 128 */
+  int out_channels;        /* 6 (eps + learned-range variance) */
+  int num_res_blocks;      /* 1 */
+  int num_levels;          /* len(channel_mult) = 6 */
+  int channel_mult[8];     /* 1,1,2,2,4,4 */
+  int num_attention;       /* number of entries in attention_ds */
+  int attention_ds[8];     /* downsample factors with attention: 16 */
+  int num_head_channels;   /* 64 */
+} ifd_config;
+
+/* Sampler coefficients: float64 on the host, rounded to fp32 once (torch semantics). */
+typedef struct ifd_step_coeffs {
+  float c_sqrt_1m_at, c_sqrt_at, c_sqrt_ap, c_dir, c_sigma;                        /* DDIM */
+  float c_min_log, c_max_log, c_recip, c_recipm1, c_coef1, c_coef2, c_nonzero;   /* DDPM */
+  float c_inj_a, c_inj_b;                                                          /* injection */
+  int use_noise, inject, clip, pad;
+} ifd_step_coeffs;
+
+typedef struct ifd_handle ifd_handle;
+
+int ifd_create(const ifd_config* cfg, ifd_handle** out);
+void ifd_destroy(ifd_handle* h);
+const char* ifd_last_error(void);
+
+/* Parameter inventory of the model (state_dict order, names without "base_model."). No GPU use. */
+int ifd_num_params(ifd_handle* h, int* n);
+int ifd_param_info(ifd_handle* h, int i, const char** name, int64_t* shape4, int* ndim);
+
+/* Copy one parameter (host or device pointer, fp32 contiguous). The handle keeps its own copy. */
+int ifd_load_weights(ifd_handle* h, const char* name, const float* data, const int64_t* shape, int ndim);
+/* Pack every loaded parameter into the device layouts. Missing parameters are an error. */
+int ifd_finalize(ifd_handle* h);
+/* Bytes of device workspace the handle holds (weights + activations). */
+int ifd_memory(ifd_handle* h, int64_t* weight_bytes, int64_t* workspace_bytes);
+
+int ifd_unet_forward(ifd_handle* h, const float* x, const float* masked_image, const float* mask,
+                     const int64_t* t, int64_t B, int H, int W, float* out6, void* stream);
+
+/* img [B,3,H,W] in/out; gt [B,3,H,W]; mask [B,1,H,W] (1 = hole); noise / known [B,3,H,W]
+ * (noise may be NULL when c->use_noise == 0 for DDIM; known may be NULL when c->inject == 0). */
+int ifd_ddim_step(ifd_handle* h, const int64_t* t, int64_t B, int H, int W, float* img, const float* gt,
+                  const float* mask, const float* noise, const float* known, const ifd_step_coeffs* c,
+                  void* stream);
+int ifd_ddpm_step(ifd_handle* h, const int64_t* t, int64_t B, int H, int W, float* img, const float* gt,
+                  const float* mask, const float* noise, const float* known, const ifd_step_coeffs* c,
+                  void* stream);
+
+int ifd_ddim_update(const float* out6, int64_t B, int H, int W, float* img, const float* gt, const float* mask,
+                    const float* noise, const float* known, const ifd_step_coeffs* c, void* stream);
+int ifd_ddpm_update(const float* out6, int64_t B, int H, int W, float* img, const float* gt, const float* mask,
+                    const float* noise, const float* known, const ifd_step_coeffs* c, void* stream);
+int ifd_blend(const float* result, const float* gt, const float* mask, int64_t B, int C, int H, int W, float* out,
+              void* stream);
+
+/* Profiling hook: time of the last forward's dominant kernel class is not tracked here; the
+ * library exposes only a version string. */
+const char* ifd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

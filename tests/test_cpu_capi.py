@@ -1,0 +1,55 @@
+"""libifd.so loads, exports every symbol of include/ifd.h, and reports the reference's parameter list
+(no GPU compute is issued here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "ifd.h")).read()
+    return sorted(set(re.findall(r"\b(ifd_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_header_symbols():
+    from ifd import _lib
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib.EXPORTS)
+
+
+@pytest.mark.parametrize("cfgname", ["REDUCED", "FULL"])
+def test_param_inventory_matches_spec(cfgname):
+    import ifd.topology as T
+    from ifd.model import Handle
+    cfg = getattr(T, cfgname)
+    h = Handle(cfg)
+    assert h.param_names() == [(k, tuple(s)) for k, s in T.state_dict_spec(cfg, prefix="")]
+
+
+def test_bad_config_is_rejected():
+    from ifd import _lib
+    L = _lib.lib()
+    c = _lib.IfdConfig()
+    c.image_size = 64
+    c.num_levels = 0
+    h = ctypes.c_void_p()
+    assert L.ifd_create(ctypes.byref(c), ctypes.byref(h)) != 0
+    assert b"unsupported" in L.ifd_last_error()
+
+
+def test_unknown_weight_name_is_an_error():
+    from ifd import _lib
+    from ifd.model import Handle
+    from ifd.topology import REDUCED
+    h = Handle(REDUCED)
+    shape = (ctypes.c_int64 * 1)(3)
+    buf = (ctypes.c_float * 3)()
+    rc = _lib.lib().ifd_load_weights(h.h, b"nope.weight", ctypes.cast(buf, ctypes.c_void_p), shape, 1)
+    assert rc != 0 and b"unexpected parameter" in _lib.lib().ifd_last_error()
