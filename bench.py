@@ -1,0 +1,203 @@
+"""Headline benchmark: 256x256 DDIM-100 inpainted images/sec on MI355X (BASELINE.json `metric`).
+
+One "step" = one full DDIM-100 inpainting pass (101 UNet evals, each with the DDIM update and the
+known-region re-injection fused into the last conv, then the final blend) over a batch of
+synthetic 256x256 inputs, per GPU. Workload = BASELINE.json configs[1]: batch 16 per GPU, DDIM-100
+cosine T=1000, eta 0.75 (code/test_inp_ddim_100.py:820), fp32, random-init weights of the
+reference architecture (seeded manifest), gt ~ U(-1,1), 25 % centre-square + random-rectangle masks.
+N GPUs = N independent shards (weak scaling), one RCCL all_gather of the outputs inside the
+timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "face-inpainting-diffusion-models_amd")]
+
+import torch  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (vector = MFMA f32), /opt/skills/guides/MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+README_S_PER_SAMPLE_DDIM100 = 3.42   # reference README.md:76 (unstated GPU, batch 4)
+
+
+def synth_inputs(B, H, seed, device):
+    g = torch.Generator().manual_seed(seed)
+    gt = torch.rand(B, 3, H, H, generator=g) * 2 - 1
+    mask = torch.zeros(B, 1, H, H)
+    q = H // 4
+    mask[:, :, q:H - q, q:H - q] = 1.0
+    for b in range(B):
+        for _ in range(2):
+            y0, x0 = [int(v) for v in torch.randint(0, H // 2, (2,), generator=g)]
+            hh, ww = [int(v) for v in torch.randint(H // 16, H // 3, (2,), generator=g)]
+            mask[b, :, y0:y0 + hh, x0:x0 + ww] = 1.0
+    return gt.to(device), mask.to(device)
+
+
+def cpu_baseline(budget_s, H=256):
+    """The oracle (pure-torch CPU restatement of the reference UNet, pinned bit-exact to it by
+    tests/golden) timed on this host's cores: B=1 256x256 UNet evals until `budget_s` elapses,
+    extrapolated x101 evals per DDIM-100 image (the update algebra is < 0.1 % of an eval)."""
+    from ifd.manifest import make_state_dict
+    from ifd.topology import FULL
+    from oracle import ref_unet
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    sd = ref_unet.strip_prefix(make_state_dict(FULL, seed=1))
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(1, 3, H, H, generator=g)
+    gt = torch.rand(1, 3, H, H, generator=g) * 2 - 1
+    mask = torch.zeros(1, 1, H, H)
+    mask[:, :, H // 4: 3 * H // 4, H // 4: 3 * H // 4] = 1
+    t = torch.tensor([500])
+    times = []
+    t_start = time.time()
+    with torch.no_grad():
+        while len(times) < 2 or (time.time() - t_start < budget_s and len(times) < 64):
+            t0 = time.time()
+            ref_unet.inpaint_forward(sd, x, t, gt * (1 - mask), mask, FULL)
+            times.append(time.time() - t0)
+    times = sorted(times[1:]) if len(times) > 2 else times
+    t_eval = times[len(times) // 2]
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": 1.0 / (101 * t_eval), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": f"{len(times)} B=1 256x256 UNet evals of oracle/ref_unet.py (torch CPU fp32), median "
+                      f"{t_eval * 1e3:.0f} ms/eval, x101 evals per DDIM-100 image",
+            "s_per_unet_eval": t_eval, "cpu_model": cpu_model}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--ddim-steps", type=int, default=100)
+    ap.add_argument("--eta", type=float, default=0.75)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    from ifd import parallel
+    from ifd.manifest import make_state_dict
+    from ifd.model import DiffusionInpaintingModel
+    from ifd.sampler import InpaintingSampler
+    from ifd.schedules import create_gaussian_diffusion
+    from ifd.topology import FULL, gflop_per_image
+    from ifd import _lib
+
+    rank, ws, local = parallel.world()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    parallel.init(device=dev)
+    B, H = args.batch, FULL.image_size
+
+    model = DiffusionInpaintingModel(FULL, device=dev)
+    model.load_state_dict(make_state_dict(FULL, seed=1))
+    model.eval()
+    diffusion = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="cosine")
+    sampler = InpaintingSampler(model, diffusion, ddim_timesteps=args.ddim_steps, device=dev)
+    gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
+    shape = (B, 3, H, H)
+    n_evals = len(sampler.create_ddim_timestep_sequence(1000, args.ddim_steps))
+    handle = model.handle(dev)
+    L = _lib.lib()
+
+    def one_pass(i):
+        torch.manual_seed(42 + 1000 * rank + i)
+        with torch.no_grad():
+            y = sampler.inpainting_ddim_sample_loop(sampler.model_fn, shape, gt, mask, True, dev, False, args.eta)
+            y = sampler.final_blend(y, gt, mask)
+            return parallel.gather_images(y, B * ws)
+
+    for i in range(args.warmup):
+        one_pass(i)
+    prof = not args.no_profile
+    if prof:
+        _lib.check(L.ifd_profile_enable(handle.h, 1))
+    parallel.barrier(dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        y = one_pass(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    parallel.barrier(dev)
+    elapsed = parallel.max_over_ranks(time.perf_counter() - t0, dev)
+    assert torch.isfinite(y).all()
+
+    roofline = None
+    kernels = {}
+    if prof:
+        buf = torch.empty(0)  # noqa: F841
+        import ctypes
+        cbuf = ctypes.create_string_buffer(1 << 16)
+        _lib.check(L.ifd_profile_report(handle.h, cbuf, len(cbuf)))
+        _lib.check(L.ifd_profile_enable(handle.h, 0))
+        kernels = json.loads(cbuf.value.decode())["kernels"]
+        conv = {k: v for k, v in kernels.items() if k.startswith("conv_kernel")}
+        dom = max(conv, key=lambda k: conv[k]["ms"])
+        d = conv[dom]
+        achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": dom,
+                    "avg_launch_ms": d["ms"] / d["count"], "flops_per_launch": d["flops"] / d["count"],
+                    "launches": int(d["count"])}
+        tot_ms = sum(v["ms"] for v in kernels.values())
+        conv_flops = sum(v["flops"] for v in conv.values())
+        conv_ms = sum(v["ms"] for v in conv.values())
+        roofline["all_conv_launches"] = {"achieved": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),
+                                         "frac": round(conv_flops / (conv_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+                                         "time_share": round(conv_ms / tot_ms, 4)}
+
+    value = B * ws * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    res = {
+        "metric": "256x256 DDIM-100 inpainted images/sec at 1/2/4/8 MI355X; per-step UNet ms",
+        "value": round(value, 4),
+        "unit": "images/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2),
+        "unet_ms_per_eval": round(ms_per_step / n_evals, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value * README_S_PER_SAMPLE_DDIM100, 2),
+        "vs_baseline_ref": "reference README.md:76: DDIM-100 3.42 s/sample (unstated GPU, batch 4)",
+        "dtype": "f32",
+        "data": "synthetic (gt~U(-1,1), centre-square + rectangle masks, seeded random-init weights)",
+        "config": {"workload": "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1])",
+                   "global_batch": B * ws, "batch_per_gpu": B, "unet_evals_per_image": n_evals,
+                   "gflop_per_unet_eval_per_image": round(gflop_per_image(FULL), 2),
+                   "parallelism": f"dp{ws} (image shards, RCCL all_gather of outputs)"},
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and ws == 1 and args.cpu_baseline_seconds > 0:
+        res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
+    if rank == 0:
+        if kernels:
+            res["kernels"] = {k: {"count": int(v["count"]), "ms": round(v["ms"], 3)} for k, v in kernels.items()}
+        print(json.dumps(res), flush=True)
+    if parallel.world()[1] > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

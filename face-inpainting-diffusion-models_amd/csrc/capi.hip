@@ -84,6 +84,20 @@ int ifd_memory(ifd_handle* h, int64_t* wb, int64_t* ws) {
   return 0;
 }
 
+int ifd_profile_enable(ifd_handle* h, int on) {
+  if (!h) { set_error("null handle"); return 2; }
+  return h->model->profile_enable(on);
+}
+
+int ifd_profile_report(ifd_handle* h, char* buf, int64_t buflen) {
+  if (!h || !buf || buflen <= 0) { set_error("ifd_profile_report: bad argument"); return 2; }
+  std::string js;
+  if (h->model->profile_report(js)) return 1;
+  if ((int64_t)js.size() + 1 > buflen) { set_error("ifd_profile_report: buffer too small"); return 2; }
+  std::memcpy(buf, js.c_str(), js.size() + 1);
+  return 0;
+}
+
 int ifd_unet_forward(ifd_handle* h, const float* x, const float* masked_image, const float* mask, const int64_t* t,
                      int64_t B, int H, int W, float* out6, void* stream) {
   if (!h || !x || !masked_image || !mask || !t || !out6) { set_error("ifd_unet_forward: null argument"); return 2; }

@@ -63,6 +63,12 @@ struct ConvParams {
   int epi;
   // tile geometry (host-computed)
   int TW, TH, IMGS, tiles_x, tiles_y;
+  int lg_tw, lg_tpi;  // log2(TW), log2(TH*TW): tile dims are powers of two
+  // split-K (low-resolution layers): blockIdx.z = split; split z accumulates main-segment chunks
+  // [z*n/S, (z+1)*n/S) (+ the 1x1 segment when z == S-1) and writes raw sums to
+  // part[z][N][H][W][cout]; splitk_reduce adds the S slabs in order, then bias and residual.
+  int ksplit;
+  float* part;
   // sampler epilogue (EPI_DDIM / EPI_DDPM): all NCHW [N,3,H,W] except mask [N,1,H,W]
   float* img; const float* gt; const float* mask; const float* noise; const float* known;
   StepCoeffs sc;
@@ -71,6 +77,9 @@ struct ConvParams {
 // Launch with the tile configuration chosen from (cout, taps, xform). Returns hipError_t.
 int launch_conv(const ConvParams& p, int taps, int xform, int bn, hipStream_t stream);
 int conv_pick_bn(int cout, int taps, int H, int W, int N);
+// Tile geometry + split-K choice shared by the launcher and the workspace planner.
+void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks);
+int launch_splitk_reduce(const ConvParams& p, hipStream_t stream);
 
 // Shared elementwise step math, also used by the standalone step kernels (sampler.hip).
 __device__ __forceinline__ float ddim_step_value(const StepCoeffs& s, float img, float eps, float noise,

@@ -8,10 +8,13 @@
 // The conv prologue (conv.hip) applies A, B (+ SiLU) while staging its input halo, so the
 // normalised tensor never goes to HBM.
 //
-// Pass 1 (gn_partial): one block per (n, slice of pixels) reads its slice once from HBM and
-// computes per group (count, mean, M2) with a two-pass (mean, then centred squares) reduction
-// over the L1/L2-resident slice — deterministic (fixed reduction tree, no atomics).
-// Pass 2 (gn_finalize): per (n, group), Chan's parallel combination in float64, then A/B.
+// Pass 1 (gn_partial): one block per (n, slice of pixels) streams its slice ONCE from HBM
+// (16-byte loads, coalesced along channels). Each thread keeps shifted sums per channel quad,
+// S1 = sum(x - K), S2 = sum((x - K)^2) with K its first sample (no cancellation: |x - K| is on the
+// scale of the group's spread), converts them to (count, mean, M2), and the block merges threads,
+// then channels of a group, with Chan's pairwise formula in a fixed order (deterministic).
+// Pass 2 (gn_finalize): one block per image; each group's slice partials are merged in float64
+// by a 32-lane tree per group, then A/B are written.
 #include "common.h"
 
 namespace ifd {
@@ -28,10 +31,21 @@ struct GnPartialParams {
   float* part;    // [N][nslices][G][3]: count, mean, M2
 };
 
+struct Stat {
+  float n, mean, m2;
+};
+
+__device__ __forceinline__ Stat merge(Stat a, Stat b) {
+  const float n = a.n + b.n;
+  if (n == 0.f) return a;
+  const float d = b.mean - a.mean;
+  const float f = b.n / n;
+  return {n, a.mean + d * f, a.m2 + b.m2 + d * d * a.n * f};
+}
+
 __global__ __launch_bounds__(GN_NT) void gn_partial_kernel(GnPartialParams p) {
-  __shared__ float red[GN_NT * 4];
-  __shared__ float chs[1024];
-  __shared__ float gmean[GN_G];
+  __shared__ Stat red[GN_NT * 4];  // [pixel lane][channel]
+  __shared__ Stat chs[1024];
   const int C = p.c0 + p.c1;
   const int QPT = C >> 2;                 // channel quads
   const int PL = GN_NT / QPT;             // pixel lanes (>= 1, C <= 1024)
@@ -48,54 +62,41 @@ __global__ __launch_bounds__(GN_NT) void gn_partial_kernel(GnPartialParams p) {
   const int Cg = C / GN_G;
   const bool active = pl < PL;
 
-  // pass 1: per-channel sums over this thread's pixels
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (active)
-    for (int px = px0 + pl; px < px1; px += PL) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + ((size_t)n * p.HW + px) * cs + co);
-      acc += v;
-    }
-  if (active) *reinterpret_cast<f32x4*>(red + 4 * (pl * QPT + q)) = acc;
-  __syncthreads();
-  for (int ch = tid; ch < C; ch += GN_NT) {
-    float t = 0.f;
-    for (int l = 0; l < PL; ++l) t += red[l * C + ch];
-    chs[ch] = t;
-  }
-  __syncthreads();
-  const float cnt = (float)(px1 - px0) * Cg;
-  if (tid < GN_G) {
-    float t = 0.f;
-    for (int j = 0; j < Cg; ++j) t += chs[tid * Cg + j];
-    gmean[tid] = t / cnt;
-  }
-  __syncthreads();
-  // pass 2: centred squares against the slice mean (re-read hits L1/L2)
-  f32x4 m2 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 K = {0.f, 0.f, 0.f, 0.f}, s1 = K, s2 = K;
+  float cnt = 0.f;
   if (active) {
-    f32x4 mu;
-    for (int j = 0; j < 4; ++j) mu[j] = gmean[(c + j) / Cg];
-    for (int px = px0 + pl; px < px1; px += PL) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + ((size_t)n * p.HW + px) * cs + co) - mu;
-      m2 += v * v;
+    const float* base = src + (size_t)n * p.HW * cs + co;
+    int px = px0 + pl;
+    if (px < px1) K = *reinterpret_cast<const f32x4*>(base + (size_t)px * cs);
+#pragma unroll 4
+    for (; px < px1; px += PL) {
+      const f32x4 d = *reinterpret_cast<const f32x4*>(base + (size_t)px * cs) - K;
+      s1 += d;
+      s2 += d * d;
+      cnt += 1.f;
+    }
+    for (int j = 0; j < 4; ++j) {
+      Stat st;
+      st.n = cnt;
+      st.mean = cnt > 0.f ? K[j] + s1[j] / cnt : 0.f;
+      st.m2 = cnt > 0.f ? fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f) : 0.f;
+      red[pl * C + c + j] = st;
     }
   }
   __syncthreads();
-  if (active) *reinterpret_cast<f32x4*>(red + 4 * (pl * QPT + q)) = m2;
-  __syncthreads();
   for (int ch = tid; ch < C; ch += GN_NT) {
-    float t = 0.f;
-    for (int l = 0; l < PL; ++l) t += red[l * C + ch];
-    chs[ch] = t;
+    Stat a = red[ch];
+    for (int l = 1; l < PL; ++l) a = merge(a, red[l * C + ch]);
+    chs[ch] = a;
   }
   __syncthreads();
   if (tid < GN_G) {
-    float t = 0.f;
-    for (int j = 0; j < Cg; ++j) t += chs[tid * Cg + j];
+    Stat a = chs[tid * Cg];
+    for (int j = 1; j < Cg; ++j) a = merge(a, chs[tid * Cg + j]);
     float* o = p.part + (((size_t)n * p.nslices + s) * GN_G + tid) * 3;
-    o[0] = cnt;
-    o[1] = gmean[tid];
-    o[2] = t;
+    o[0] = a.n;
+    o[1] = a.mean;
+    o[2] = a.m2;
   }
 }
 
@@ -109,24 +110,40 @@ struct GnFinalizeParams {
   float* A; float* B;  // [N][C]
 };
 
+// 256 threads = 8 groups x 32 lanes per pass; each lane merges a strided subset of the slices in
+// float64, then a fixed 5-level butterfly merges the 32 lanes (deterministic).
 __global__ __launch_bounds__(GN_NT) void gn_finalize_kernel(GnFinalizeParams p) {
   __shared__ float smean[GN_G], srstd[GN_G];
   const int n = blockIdx.x, tid = threadIdx.x;
-  if (tid < GN_G) {
+  const int lane = tid & 31, gsub = tid >> 5;
+  for (int g = gsub; g < GN_G; g += GN_NT / 32) {
     double cnt = 0.0, mean = 0.0, m2 = 0.0;
-    for (int s = 0; s < p.nslices; ++s) {
-      const float* o = p.part + (((size_t)n * p.nslices + s) * GN_G + tid) * 3;
+    for (int s = lane; s < p.nslices; s += 32) {
+      const float* o = p.part + (((size_t)n * p.nslices + s) * GN_G + g) * 3;
       const double nb = o[0], mb = o[1], m2b = o[2];
       if (nb <= 0) continue;
-      const double tot = cnt + nb;
-      const double d = mb - mean;
+      const double tot = cnt + nb, d = mb - mean;
       mean += d * (nb / tot);
       m2 += m2b + d * d * (cnt * nb / tot);
       cnt = tot;
     }
-    const double var = m2 / cnt;
-    smean[tid] = (float)mean;
-    srstd[tid] = (float)(1.0 / sqrt(var + (double)p.eps));
+    for (int off = 16; off > 0; off >>= 1) {
+      const double nb = __shfl_xor(cnt, off, 32), mb = __shfl_xor(mean, off, 32), m2b = __shfl_xor(m2, off, 32);
+      const double tot = cnt + nb;
+      if (tot > 0) {
+        // symmetric form so both lanes of a pair compute the same value
+        const double lo_n = (lane & off) ? nb : cnt, lo_m = (lane & off) ? mb : mean, lo_2 = (lane & off) ? m2b : m2;
+        const double hi_n = (lane & off) ? cnt : nb, hi_m = (lane & off) ? mean : mb, hi_2 = (lane & off) ? m2 : m2b;
+        const double d = hi_m - lo_m;
+        mean = lo_m + d * (hi_n / tot);
+        m2 = lo_2 + hi_2 + d * d * (lo_n * hi_n / tot);
+        cnt = tot;
+      }
+    }
+    if (lane == 0) {
+      smean[g] = (float)mean;
+      srstd[g] = (float)(1.0 / sqrt(m2 / cnt + (double)p.eps));
+    }
   }
   __syncthreads();
   const int Cg = p.C / GN_G;
@@ -146,8 +163,10 @@ __global__ __launch_bounds__(GN_NT) void gn_finalize_kernel(GnFinalizeParams p) 
   }
 }
 
+// Pixels per partial block: large enough to stream (>= 1024 pixels where possible), small enough
+// that B x slices fills the chip.
 int gn_slices(int HW, int* slice) {
-  int s = HW < 256 ? HW : 256;
+  int s = HW < 1024 ? HW : 1024;
   *slice = s;
   return (HW + s - 1) / s;
 }

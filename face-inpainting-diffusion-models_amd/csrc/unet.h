@@ -64,6 +64,9 @@ class Model {
               int epi, float* out6, const StepCoeffs* sc, float* img, const float* gt, const float* mask,
               const float* noise, const float* known, hipStream_t s);
   int64_t weight_bytes() const { return (int64_t)wblob_floats_ * 4; }
+  // Event-based per-launch profiler (records on the launch stream; read after a sync).
+  int profile_enable(int on);
+  int profile_report(std::string& json);
   int64_t workspace_bytes() const { return (int64_t)ws_floats_ * 4; }
 
  private:
@@ -78,6 +81,20 @@ class Model {
                const float* res, int res_xf, int resH, float* out, int epi, hipStream_t s,
                const StepCoeffs* sc = nullptr, float* img = nullptr, const float* gt = nullptr,
                const float* mask = nullptr, const float* noise = nullptr, const float* known = nullptr);
+
+  struct ProfRec {
+    std::string name;
+    double flops, bytes;
+    hipEvent_t e0, e1;
+  };
+  bool prof_on_ = false;
+  bool prof_layers_ = false;  // profile_enable(h, 2): key conv launches by layer shape
+  std::vector<ProfRec> prof_;
+  std::vector<hipEvent_t> ev_pool_;
+  size_t ev_used_ = 0;
+  hipEvent_t take_event();
+  void prof_begin(hipStream_t s, hipEvent_t* e0);
+  void prof_end(hipStream_t s, hipEvent_t e0, const std::string& name, double flops, double bytes);
 
   ifd_config cfg_;
   std::vector<ParamSpec> params_;
@@ -103,7 +120,8 @@ class Model {
   int ws_B_ = 0;
   // workspace carve (float offsets), valid for ws_B_
   size_t o_x0_ = 0, o_bufs_[3] = {0, 0, 0}, o_t1_ = 0, o_qkv_ = 0, o_ao_ = 0, o_A_ = 0, o_B_ = 0, o_part_ = 0,
-         o_emb_ = 0, o_E_ = 0;
+         o_emb_ = 0, o_E_ = 0, o_split_ = 0;
+  size_t split_floats_ = 0;
   std::vector<size_t> o_hs_;
 };
 

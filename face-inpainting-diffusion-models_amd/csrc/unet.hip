@@ -8,6 +8,8 @@
 #include "unet.h"
 
 #include <algorithm>
+#include <array>
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 
@@ -20,6 +22,66 @@ Model::Model(const ifd_config& cfg) : cfg_(cfg) { build_plan(); }
 Model::~Model() {
   if (wblob_) (void)hipFree(wblob_);
   if (ws_) (void)hipFree(ws_);
+  for (auto e : ev_pool_) (void)hipEventDestroy(e);
+}
+
+hipEvent_t Model::take_event() {
+  if (ev_used_ == ev_pool_.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    ev_pool_.push_back(e);
+  }
+  return ev_pool_[ev_used_++];
+}
+
+void Model::prof_begin(hipStream_t s, hipEvent_t* e0) {
+  *e0 = nullptr;
+  if (!prof_on_) return;
+  *e0 = take_event();
+  if (*e0) (void)hipEventRecord(*e0, s);
+}
+
+void Model::prof_end(hipStream_t s, hipEvent_t e0, const std::string& name, double flops, double bytes) {
+  if (!prof_on_ || !e0) return;
+  hipEvent_t e1 = take_event();
+  if (!e1) return;
+  (void)hipEventRecord(e1, s);
+  prof_.push_back({name, flops, bytes, e0, e1});
+}
+
+int Model::profile_enable(int on) {
+  prof_on_ = on != 0;
+  prof_layers_ = on == 2;
+  prof_.clear();
+  ev_used_ = 0;
+  return 0;
+}
+
+// JSON: {"kernels": {name: {"count", "ms", "flops", "bytes"}}}; call after the stream is synchronised.
+int Model::profile_report(std::string& json) {
+  std::map<std::string, std::array<double, 4>> agg;
+  for (auto& r : prof_) {
+    float ms = 0.f;
+    IFD_CHECK_HIP(hipEventElapsedTime(&ms, r.e0, r.e1));
+    auto& a = agg[r.name];
+    a[0] += 1;
+    a[1] += ms;
+    a[2] += r.flops;
+    a[3] += r.bytes;
+  }
+  json = "{\"kernels\": {";
+  bool first = true;
+  for (auto& kv : agg) {
+    char buf[512];
+    snprintf(buf, sizeof(buf), "%s\"%s\": {\"count\": %.0f, \"ms\": %.6f, \"flops\": %.6e, \"bytes\": %.6e}",
+             first ? "" : ", ", kv.first.c_str(), kv.second[0], kv.second[1], kv.second[2], kv.second[3]);
+    json += buf;
+    first = false;
+  }
+  json += "}}";
+  prof_.clear();
+  ev_used_ = 0;
+  return 0;
 }
 
 void Model::add_param(const std::string& n, std::vector<int64_t> shape) { params_.push_back({n, std::move(shape)}); }
@@ -373,6 +435,27 @@ int Model::ensure_workspace(int B) {
   int slice;
   const int nsl = gn_slices(R * R, &slice);
   o_part_ = reserve((size_t)B * nsl * 32 * 3);
+  // split-K slabs: worst case over every conv of the plan at this batch
+  split_floats_ = 0;
+  auto consider = [&](const ConvW& cw, int H) {
+    ConvParams g;
+    std::memset(&g, 0, sizeof(g));
+    g.cout_pad = cw.cout_pad;
+    conv_geometry(g, H, H, B, cw.bn, cw.cin_pad / 8);
+    if (g.ksplit > 1) split_floats_ = std::max(split_floats_, (size_t)g.ksplit * B * H * H * cw.cout);
+  };
+  for (auto& r : res_) {
+    for (int H = 2; H <= R; H *= 2) {  // resolution is not stored per ResBlock: bound over all sizes
+      consider(r.conv1, H);
+      consider(r.conv2, H);
+    }
+  }
+  for (auto& a : attn_)
+    for (int H = 2; H <= R; H *= 2) {
+      consider(a.qkv, H);
+      consider(a.proj, H);
+    }
+  o_split_ = reserve(std::max<size_t>(split_floats_, 64));
   o_emb_ = reserve((size_t)B * emb_dim_);
   o_E_ = reserve((size_t)B * emb_total_);
   if (ws_) IFD_CHECK_HIP(hipFree(ws_));
@@ -404,22 +487,42 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   p.res = res; p.res_xform = res_xf; p.res_H = resH; p.res_W = resH;
   p.out = out;
   p.epi = epi;
-  p.TW = std::min(H, 32);
-  p.TH = std::min(H, 128 / p.TW);
-  p.IMGS = 128 / (p.TH * p.TW);
-  p.tiles_x = H / p.TW;
-  p.tiles_y = H / p.TH;
+  IFD_REQUIRE((H & (H - 1)) == 0, "spatial size must be a power of two");
+  conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8);
+  if (epi != EPI_NHWC) p.ksplit = 1;
+  p.part = ws_ + o_split_;
+  IFD_REQUIRE(p.ksplit == 1 || (size_t)p.ksplit * N * H * H * cw.cout <= split_floats_, "split-K workspace");
   if (sc) p.sc = *sc;
   p.img = img; p.gt = gt; p.mask = mask; p.noise = noise; p.known = known;
   IFD_REQUIRE(c0 % 8 == 0 && c1 % 8 == 0 && c0 + c1 == cw.cin_pad, "conv input channels");
   IFD_REQUIRE(!cw.has_skip || (sc0 + sc1 == cw.cs_pad && sc0 % 8 == 0 && sc1 % 8 == 0), "skip channels");
+  hipEvent_t e0;
+  prof_begin(s, &e0);
   int e = launch_conv(p, cw.taps, xf, cw.bn, s);
+  if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, s);
+  if (prof_on_) {
+    // algorithmic work: 2*MAC over real channels; bytes = activations in + weights + out (once each)
+    const int cin_real = (&cw == &conv_in_) ? cfg_.in_channels : cw.cin;
+    const double pix = (double)N * H * H;
+    const double flops = 2.0 * pix * cw.cout * ((double)cw.taps * cin_real + (cw.has_skip ? cw.cs : 0));
+    const double bytes = 4.0 * ((double)N * Hin * Hin * (c0 + c1) + pix * cw.cout + (double)cw.cout * cw.cin * cw.taps +
+                                (cw.has_skip ? pix * cw.cs : 0) + (res ? pix * cw.cout : 0));
+    char nm[160];
+    if (prof_layers_)
+      snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%d> r%d %d+%d->%d skip%d", cw.bn, cw.taps, xf, H, c0, c1, cw.cout,
+               cw.has_skip ? cw.cs : 0);
+    else
+      snprintf(nm, sizeof(nm), "conv_kernel<%d,%s,%d,%d>", cw.bn, cw.bn == 32 ? "4,1" : "2,2", cw.taps, xf);
+    prof_end(s, e0, nm, flops, bytes);
+  }
   if (e) {
     set_error(std::string("conv launch failed: ") + hipGetErrorString((hipError_t)e));
     return 1;
   }
   return 0;
 }
+
+static double gn_bytes(int N, int HW, int C) { return 4.0 * 2.0 * N * (double)HW * C; }
 
 int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, int c1, int N, int Hin, float* out,
                    hipStream_t s) {
@@ -428,14 +531,19 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
   float* part = ws_ + o_part_;
   float* t1 = ws_ + o_t1_;
   const int H = r.xf == XF_UP ? 2 * Hin : (r.xf == XF_DOWN ? Hin / 2 : Hin);
+  hipEvent_t g0;
+  prof_begin(s, &g0);
   int e = launch_gn(in0, c0, in1, c1, N, Hin * Hin, wblob_ + r.gn1.g_off, wblob_ + r.gn1.b_off, nullptr, 0, 0, part, A,
                     Bc, s);
+  prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, Hin * Hin, c0 + c1));
   IFD_REQUIRE(e == 0, "gn launch");
   if (run_conv(r.conv1, in0, c0, in1, c1, N, Hin, H, r.xf, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
                0, t1, EPI_NHWC, s))
     return 1;
+  prof_begin(s, &g0);
   e = launch_gn(t1, r.cout, nullptr, 0, N, H * H, wblob_ + r.gn2.g_off, wblob_ + r.gn2.b_off, ws_ + o_E_, emb_total_,
                 r.emb_off, part, A, Bc, s);
+  prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, H * H, r.cout));
   IFD_REQUIRE(e == 0, "gn launch");
   const float* res = r.conv2.has_skip ? nullptr : in0;
   return run_conv(r.conv2, t1, r.cout, nullptr, 0, N, H, H, XF_NONE, ACT_AFFINE_SILU, A, Bc, in0, c0, in1, c1, res,
@@ -448,15 +556,20 @@ int Model::run_attn(const AttnP& a, const float* in, int N, int Hin, float* out,
   float* qkv = ws_ + o_qkv_;
   float* ao = ws_ + o_ao_;
   const int T = Hin * Hin;
+  hipEvent_t g0;
+  prof_begin(s, &g0);
   int e = launch_gn(in, a.C, nullptr, 0, N, T, wblob_ + a.gn.g_off, wblob_ + a.gn.b_off, nullptr, 0, 0,
                     ws_ + o_part_, A, Bc, s);
+  prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, T, a.C));
   IFD_REQUIRE(e == 0, "gn launch");
   if (run_conv(a.qkv, in, a.C, nullptr, 0, N, Hin, Hin, XF_NONE, ACT_AFFINE, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
                0, qkv, EPI_NHWC, s))
     return 1;
   const float scale = (float)(1.0 / std::sqrt(std::sqrt((double)cfg_.num_head_channels)));
   IFD_REQUIRE(cfg_.num_head_channels == 64, "attention kernel is specialised for 64-channel heads");
+  prof_begin(s, &g0);
   launch_attention(qkv, N, T, a.C, scale, ao, s);
+  prof_end(s, g0, "attention_kernel", 4.0 * N * (double)T * T * a.C, 4.0 * N * (double)T * a.C * 4);
   return run_conv(a.proj, ao, a.C, nullptr, 0, N, Hin, Hin, XF_NONE, ACT_NONE, nullptr, nullptr, nullptr, 0, nullptr,
                   0, in, XF_NONE, Hin, out, EPI_NHWC, s);
 }
@@ -473,10 +586,14 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   const int R = cfg_.image_size;
   const int mc = cfg_.model_channels;
   float* x0 = ws_ + o_x0_;
+  hipEvent_t p0;
+  prof_begin(s, &p0);
   launch_pack_input(x, a, m, pack_mode, B, R * R, x0, s);
   launch_temb(t, wblob_ + freqs_, mc, wblob_ + te_w0_, wblob_ + te_b0_, wblob_ + te_w2_, wblob_ + te_b2_, emb_dim_, B,
               ws_ + o_emb_, s);
   launch_emb_proj(ws_ + o_emb_, emb_dim_, B, wblob_ + embw_, wblob_ + embb_, emb_total_, ws_ + o_E_, s);
+  prof_end(s, p0, "input_pack+temb+emb_proj", 2.0 * B * (double)emb_dim_ * (mc + emb_dim_ + emb_total_),
+           4.0 * B * (double)R * R * (7 + 16) + 4.0 * emb_dim_ * (double)emb_total_);
 
   // input blocks
   if (run_conv(conv_in_, x0, 16, nullptr, 0, B, R, R, XF_NONE, ACT_NONE, nullptr, nullptr, nullptr, 0, nullptr, 0,
@@ -545,8 +662,10 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   // out: GN -> SiLU -> conv 3x3 -> [B,6,H,W] (or the fused sampler update)
   float* A = ws_ + o_A_;
   float* Bc = ws_ + o_B_;
+  prof_begin(s, &p0);
   int e = launch_gn(cur, cur_c, nullptr, 0, B, R * R, wblob_ + gn_out_.g_off, wblob_ + gn_out_.b_off, nullptr, 0, 0,
                     ws_ + o_part_, A, Bc, s);
+  prof_end(s, p0, "groupnorm_stats", 0.0, gn_bytes(B, R * R, cur_c));
   IFD_REQUIRE(e == 0, "gn launch");
   return run_conv(conv_out_, cur, cur_c, nullptr, 0, B, R, R, XF_NONE, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0,
                   nullptr, 0, 0, out6, epi, s, sc, img, gt, mask, noise, known);

@@ -91,8 +91,11 @@ int ifd_ddpm_update(const float* out6, int64_t B, int H, int W, float* img, cons
 int ifd_blend(const float* result, const float* gt, const float* mask, int64_t B, int C, int H, int W, float* out,
               void* stream);
 
-/* Profiling hook: time of the last forward's dominant kernel class is not tracked here; the
- * library exposes only a version string. */
+/* Per-launch profiler: when enabled, every kernel the handle launches is bracketed by hipEvents on
+ * its stream; after the caller synchronises, ifd_profile_report writes a JSON summary per kernel
+ * name {"count", "ms", "flops" (algorithmic 2*MAC), "bytes" (algorithmic)} and clears it. */
+int ifd_profile_enable(ifd_handle* h, int on);  /* 0 off, 1 by kernel, 2 by kernel + layer shape */
+int ifd_profile_report(ifd_handle* h, char* buf, int64_t buflen);
 const char* ifd_version(void);
 
 #ifdef __cplusplus

@@ -3,10 +3,10 @@
 Tolerances (fp32 throughout; the GPU convs sum in a different order than oneDNN):
   * one UNet eval:                    max-abs <= 2e-5 (outputs are O(1), std ~0.15)
   * update kernels vs oracle algebra: DDIM bit-exact; DDPM <= 2e-6 (expf ulp differences)
-  * full loops:                       max-abs < 1e-4 (north_star), except the 10-step cosine
-                                      schedule whose first jump amplifies eval rounding ~3e3x:
-                                      documented bound 1e-3 (SURVEY §7 "Parity under error
-                                      amplification").
+  * full loops:                       max-abs < 1e-4 (north_star), except the 256x256 10-step
+                                      cosine C1 loops, whose first jump amplifies eval rounding
+                                      ~1e4x at isolated pixels: bounded by the oracle's own
+                                      perturbation envelope (test_script_ddim_full_c1).
 """
 import os
 
@@ -237,17 +237,22 @@ def test_library_loops(loops, meta, red_model, name):
 @pytest.mark.parametrize("name", ["c1_full_cos10_eta0.9", "c1_full_cos10_eta0"])
 def test_script_ddim_full_c1(loops, meta, full_model, name):
     """C1 (256x256, 10-step cosine): the first jump 999->900 divides eps by sqrt(abar_999) = 4.9e-5,
-    so pixels near the x0 clamp boundary amplify any eval rounding difference ~1e4x. The bound is
-    the oracle's OWN spread under a 1e-6 relative perturbation of eps (tests/golden/conditioning.py):
-    max-abs <= max(1e-3, 2 x that spread), and the 99.9th percentile error < 1e-4."""
+    so the few pixels near the x0 clamp boundary amplify ANY eval rounding difference ~1e4x.
+    Bound = the oracle's OWN envelope when its eps is perturbed by a relative 1e-5 (our per-eval
+    deviation from oneDNN is <= ~1e-5 relative; tests/golden/conditioning.py): max-abs within that
+    envelope's max, the fraction of pixels off by > 1e-4 within its fraction, and the 99.9th
+    percentile < 1e-4."""
     import json
     cond = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "conditioning.json")))
-    spread = max(v["max"] for k, v in cond.items() if k.startswith(name + "/rel1e-06"))
+    env = [v for k, v in cond.items() if k.startswith(name + "/rel1e-05")]
+    env_max = max(v["max"] for v in env)
+    env_frac = max(v["frac_gt_1e-4"] for v in env)
     lm = meta["loops"][name]
     gt, mask = _t(loops[f"{name}/gt"]), _t(loops[f"{name}/mask"])
     y = _run_script_loop(full_model, lm, gt, mask)
     d = (y.double().cpu() - _t(loops[f"{name}/y"]).double()).abs().flatten()
-    err, p999 = float(d.max()), float(d.quantile(0.999))
-    tol = max(1e-3, 2 * spread)
-    print(f"{name}: maxabs={err:.3g} p99.9={p999:.3g} (tol {tol:.3g}; oracle 1e-6 spread {spread:.3g})")
-    assert err <= tol and p999 < 1e-4
+    err, p999, frac = float(d.max()), float(d.quantile(0.999)), float((d > 1e-4).double().mean())
+    tol = max(1e-3, env_max)
+    print(f"{name}: maxabs={err:.3g} p99.9={p999:.3g} frac>1e-4={frac:.2e} "
+          f"(envelope max {env_max:.3g}, frac {env_frac:.2e})")
+    assert err <= tol and p999 < 1e-4 and frac <= max(env_frac, 1e-5)
