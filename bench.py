@@ -156,7 +156,7 @@ def main():
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": dom,
                     "avg_launch_ms": d["ms"] / d["count"], "flops_per_launch": d["flops"] / d["count"],
-                    "launches": int(d["count"])}
+                    "algorithmic_bytes_per_launch": d["bytes"] / d["count"], "launches": int(d["count"])}
         tot_ms = sum(v["ms"] for v in kernels.values())
         conv_flops = sum(v["flops"] for v in conv.values())
         conv_ms = sum(v["ms"] for v in conv.values())

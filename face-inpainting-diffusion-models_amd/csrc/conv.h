@@ -62,7 +62,8 @@ struct ConvParams {
   float* out;
   int epi;
   // tile geometry (host-computed)
-  int TW, TH, IMGS, tiles_x, tiles_y;
+  int bm;  // pixel-tile size (128 or 256), chosen by conv_geometry
+  int TW, TH, IMGS, tiles_x, tiles_y, npix_tiles;
   int lg_tw, lg_tpi;  // log2(TW), log2(TH*TW): tile dims are powers of two
   // split-K (low-resolution layers): blockIdx.z = split; split z accumulates main-segment chunks
   // [z*n/S, (z+1)*n/S) (+ the 1x1 segment when z == S-1) and writes raw sums to

@@ -1,7 +1,8 @@
 // Fused implicit-GEMM 3x3 / 1x1 convolution for gfx950 (see conv.h for the operator contract).
 //
-// GEMM view: M = output pixels (128-pixel tile = IMGS x TH x TW, TW = min(W, 32)),
-//            N = output channels (BN tile), K = (tap, input channel) in chunks of 8 channels.
+// GEMM view: M = output pixels (BM-pixel tile = IMGS x TH x TW, TW = min(W, 32); BM = 256 for the
+//            high-resolution layers, 128 otherwise), N = output channels (BN = 64, 32 for the
+//            6-channel head), K = (tap, input channel) in chunks of 8 channels.
 // Per K-chunk the block stages into LDS
 //   * the activated input halo  A[q][pixel][4]   (q = channel quad 0/1, (TH+2) x (TW+2) halo per image)
 //   * the packed weight slab    W[tap][q][co][4]
@@ -11,16 +12,27 @@
 //   * waves 0-3 are CONSUMERS: only ds_read_b128 + v_mfma_f32_32x32x2_f32. Each owns a
 //     (32*MR) x (32*NR) sub-tile; per tap it reads one A fragment per 32-pixel block and one B
 //     fragment per 32-channel block and issues 4 MFMAs per block pair (MFMA j consumes element j:
-//     K = {channel j (lanes 0-31), channel 4+j (lanes 32-63)}).
-//   * waves 4-7 are PRODUCERS: global loads of chunk k+1, the prologue (GroupNorm-apply [+ scale/
-//     shift] + SiLU, nearest-up / avg-pool resample, zero padding) and the LDS writes.
-// A producer and a consumer share each SIMD: the VALU/LDS-write work of the producer issues
-// beside the consumer's MFMAs (separate pipes), so the prologue costs no matrix-core time.
-// One __syncthreads per chunk hands buffer k&1 to the consumers and (k+1)&1 to the producers.
+//     K = {channel j (lanes 0-31), channel 4+j (lanes 32-63)}). The next tap's fragment reads are
+//     pinned after the first MFMA group (sched_group_barrier) so their latency hides.
+//   * waves 4-7 are PRODUCERS: global loads of chunk k+2 (two register sets in flight), the
+//     prologue of chunk k+1 (GroupNorm-apply [+ scale/shift] + SiLU, nearest-up / avg-pool
+//     resample, zero padding) and its LDS writes.
+// A producer and a consumer share each SIMD: the producer's VALU/LDS-write work issues beside the
+// consumer's MFMAs (separate pipes). One __syncthreads per chunk hands buffer k&1 to the consumers
+// and (k+1)&1 to the producers. Ablation (IFD_ABLATE=1: producers idle) shows the consumer/barrier
+// structure alone reaches ~94% of the fp32 MFMA peak; the producer's global-load stream (weights:
+// 9*8*BN floats per chunk, reused by BM pixels) is what BM = 256 amortises.
 // fp32 in / fp32 accumulate: the MFMA result is an exact fp32 fma chain (no reduced precision).
 #include "conv.h"
 
 #include <cstdlib>
+
+// Timing-only ablation builds (never shipped; outputs are garbage):
+//   IFD_ABLATE=1  producers skip every load / store (barriers only)
+//   IFD_ABLATE=2  consumers skip the fragment ds_reads (MFMAs on stale registers)
+#ifndef IFD_ABLATE
+#define IFD_ABLATE 0
+#endif
 
 namespace ifd {
 
@@ -35,17 +47,17 @@ __device__ __forceinline__ f32x4 gld4(const float* p) { return *(glb_f4*)(p); }
 __device__ __forceinline__ float gld1(const float* p) { return *(glb_f*)(p); }
 __device__ __forceinline__ void gst1(float* p, float v) { *(__attribute__((address_space(1))) float*)(p) = v; }
 
-constexpr int BM = 128;
-constexpr int NT = 512;           // threads per block
-constexpr int NP_T = 256;         // producer threads (waves 4-7)
-constexpr int MAX_HALO_ITEMS = 4;  // 2 * NP <= 1024 (NP = 512 only for 2x2 images)
+constexpr int NT = 512;    // threads per block
+constexpr int NP_T = 256;  // producer threads (waves 4-7)
 
-// SiLU of the GroupNorm-applied value, x / (1 + exp(-x)) with IEEE division and a 1-ulp expf as
-// torch's CPU kernel. It runs on the producer waves, beside the MFMAs, so accuracy costs no
-// matrix-core time.
-__device__ __forceinline__ float silu_fast(float x) { return x / (1.0f + expf(-x)); }
+// SiLU of the GroupNorm-applied value: x * rcp(1 + 2^(-x*log2 e)) on v_exp_f32 / v_rcp_f32
+// (relative error < 1e-6 for |x| < 10 against torch's x / (1 + exp(-x)); a whole UNet eval stays
+// at ~2e-6 max-abs from the reference). The producer waves bound the pipeline, so the short form.
+__device__ __forceinline__ float silu_fast(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
 
-template <int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN>
 struct Tile {
   static constexpr int MR = BM / WGM / 32;
   static constexpr int NR = BN / WGN / 32;
@@ -53,10 +65,10 @@ struct Tile {
   static_assert(WGM * WGN == 4, "4 consumer waves");
 };
 
-template <int BN, int WGM, int WGN>
-using AccArr = f32x16[Tile<BN, WGM, WGN>::MR][Tile<BN, WGM, WGN>::NR];
-template <int BN, int WGM, int WGN>
-using PixArr = int[Tile<BN, WGM, WGN>::MR];
+template <int BM, int BN, int WGM, int WGN>
+using AccArr = f32x16[Tile<BM, BN, WGM, WGN>::MR][Tile<BM, BN, WGM, WGN>::NR];
+template <int BM, int BN, int WGM, int WGN>
+using PixArr = int[Tile<BM, BN, WGM, WGN>::MR];
 
 struct SegSrc {
   const float* p0; int c0;
@@ -69,15 +81,14 @@ struct HaloItem {
   int srcpix;   // source pixel index n*Hs*Ws + sy*Ws + sx (top-left for XF_DOWN); 0 if invalid
   int n;        // image index (activation coefficients)
   int ldsoff;   // float offset in the A buffer, -1 if this item slot is unused
-  int quad;     // channel quad 0/1
 };
 
-template <int TAPS, int XF>
-__device__ __forceinline__ void make_items(HaloItem (&it)[MAX_HALO_ITEMS], int ptid, int NP, int HHd, int HWd,
-                                           int n0, int y0, int x0, int N, int H, int W, int Hs, int Ws) {
+template <int TAPS, int XF, int MAXI>
+__device__ __forceinline__ void make_items(HaloItem (&it)[MAXI], int ptid, int NP, int HHd, int HWd, int n0, int y0,
+                                           int x0, int N, int H, int W, int Hs, int Ws) {
   constexpr int HALO = (TAPS == 9) ? 1 : 0;
 #pragma unroll
-  for (int k = 0; k < MAX_HALO_ITEMS; ++k) {
+  for (int k = 0; k < MAXI; ++k) {
     const int idx = ptid + k * NP_T;
     const int q = idx & 1, pix = idx >> 1;
     const int per = HHd * HWd;
@@ -92,45 +103,55 @@ __device__ __forceinline__ void make_items(HaloItem (&it)[MAX_HALO_ITEMS], int p
     it[k].srcpix = inb ? (n * Hs + sy) * Ws + sx : 0;
     it[k].n = inb ? n : 0;
     it[k].ldsoff = idx < 2 * NP ? (q * NP + pix) * 4 : -1;
-    it[k].quad = q;
   }
 }
 
-template <int BN, int TAPS, int XF>
+// Producer register set for one chunk. Every item of a thread has the same channel quad
+// (ptid & 1, since NP_T is even); with ONEIMG (tile = one image) they also share the image, so
+// one GroupNorm coefficient pair per thread per chunk replaces one per item.
+template <int BN, int TAPS, int XF, int MAXI, bool ONEIMG>
 struct Producer {
   static constexpr int NSRC = (XF == XF_DOWN) ? 4 : 1;
+  static constexpr int NCO = ONEIMG ? 1 : MAXI;
   static constexpr int WITEMS = (TAPS * 2 * BN + NP_T - 1) / NP_T;
   static constexpr bool WEXACT = (TAPS * 2 * BN) % NP_T == 0;
 
-  f32x4 raw[MAX_HALO_ITEMS][NSRC];
-  f32x4 ca[MAX_HALO_ITEMS], cb[MAX_HALO_ITEMS];
+  f32x4 raw[MAXI][NSRC];
+  f32x4 ca[NCO], cb[NCO];
   f32x4 wr[WITEMS];
 
   // Issue the global loads of chunk k into registers (branch-free: invalid items read pixel 0).
-  __device__ __forceinline__ void load(const HaloItem (&it)[MAX_HALO_ITEMS], int nitems, int ptid, const SegSrc& s,
-                                       int k, int act, const float* actA, const float* actB, int ctot,
-                                       const float* wslab, int Ws) {
+  __device__ __forceinline__ void load(const HaloItem (&it)[MAXI], int nitems, int ptid, const SegSrc& s, int k,
+                                       int act, const float* actA, const float* actB, int ctot, const float* wslab,
+                                       int Ws, int n0) {
+    if (IFD_ABLATE == 1) return;
     const int cb0 = 8 * k;
     const bool first = cb0 < s.c0;
     const float* src = first ? s.p0 : s.p1;
     const int cs = first ? s.c0 : s.c1;
-    const int coff = first ? cb0 : cb0 - s.c0;
+    const int quad = ptid & 1;
+    const int coff = (first ? cb0 : cb0 - s.c0) + 4 * quad;
 #pragma unroll
-    for (int i = 0; i < MAX_HALO_ITEMS; ++i) {
+    for (int i = 0; i < MAXI; ++i) {
       if (i < nitems) {
-        const float* base = src + (size_t)it[i].srcpix * cs + coff + 4 * it[i].quad;
+        const float* base = src + (size_t)it[i].srcpix * cs + coff;
         raw[i][0] = gld4(base);
         if (XF == XF_DOWN) {
           raw[i][1] = gld4(base + cs);
           raw[i][2] = gld4(base + (size_t)Ws * cs);
           raw[i][3] = gld4(base + (size_t)Ws * cs + cs);
         }
-        if (act != ACT_NONE) {
-          const int ci = it[i].n * ctot + cb0 + 4 * it[i].quad;
+        if (!ONEIMG && act != ACT_NONE) {
+          const int ci = it[i].n * ctot + cb0 + 4 * quad;
           ca[i] = gld4(actA + ci);
           cb[i] = gld4(actB + ci);
         }
       }
+    }
+    if (ONEIMG && act != ACT_NONE) {
+      const int ci = n0 * ctot + cb0 + 4 * quad;
+      ca[0] = gld4(actA + ci);
+      cb[0] = gld4(actB + ci);
     }
 #pragma unroll
     for (int i = 0; i < WITEMS; ++i) {
@@ -146,24 +167,26 @@ struct Producer {
   }
 
   // Apply the prologue (act, resample, zero padding) and write the chunk into LDS.
-  __device__ __forceinline__ void store(const HaloItem (&it)[MAX_HALO_ITEMS], int nitems, int ptid, int act,
-                                        lds_f* As, lds_f* Ws_) {
+  __device__ __forceinline__ void store(const HaloItem (&it)[MAXI], int nitems, int ptid, int act, lds_f* As,
+                                        lds_f* Ws_) {
+    if (IFD_ABLATE == 1) return;
 #pragma unroll
-    for (int i = 0; i < MAX_HALO_ITEMS; ++i) {
+    for (int i = 0; i < MAXI; ++i) {
       if (i < nitems && it[i].ldsoff >= 0) {
+        const int c = ONEIMG ? 0 : i;
         f32x4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float r;
           if (XF == XF_DOWN) {
             // AvgPool2d(2,2) of the activated tensor: ((v00 + v01) + v10) + v11, then / 4
-            float s = act1(raw[i][0][j], ca[i][j], cb[i][j], act);
-            s = s + act1(raw[i][1][j], ca[i][j], cb[i][j], act);
-            s = s + act1(raw[i][2][j], ca[i][j], cb[i][j], act);
-            s = s + act1(raw[i][3][j], ca[i][j], cb[i][j], act);
+            float s = act1(raw[i][0][j], ca[c][j], cb[c][j], act);
+            s = s + act1(raw[i][1][j], ca[c][j], cb[c][j], act);
+            s = s + act1(raw[i][2][j], ca[c][j], cb[c][j], act);
+            s = s + act1(raw[i][3][j], ca[c][j], cb[c][j], act);
             r = s * 0.25f;
           } else {
-            r = act1(raw[i][0][j], ca[i][j], cb[i][j], act);
+            r = act1(raw[i][0][j], ca[c][j], cb[c][j], act);
           }
           v[j] = r * it[i].valid;  // zero padding after the activation (and for tail images)
         }
@@ -178,38 +201,59 @@ struct Producer {
   }
 };
 
-// MFMAs over one staged chunk (consumer waves).
-template <int BN, int WGM, int WGN, int TAPS>
-__device__ __forceinline__ void consume(AccArr<BN, WGM, WGN>& acc, const lds_f* As, const lds_f* Ws_, int NP, int HWd,
-                                        const PixArr<BN, WGM, WGN>& pb, int wn0) {
-  using T = Tile<BN, WGM, WGN>;
+// MFMAs over one staged chunk (consumer waves). Fragment reads are software-pipelined one tap
+// ahead (two register slots, fully unrolled so the slots are static).
+template <int BM, int BN, int WGM, int WGN, int TAPS>
+__device__ __forceinline__ void consume(AccArr<BM, BN, WGM, WGN>& acc, const lds_f* As, const lds_f* Ws_, int NP,
+                                        int HWd, const PixArr<BM, BN, WGM, WGN>& pb, int wn0) {
+  using T = Tile<BM, BN, WGM, WGN>;
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const lds_f* Ab = As + 4 * h * NP;
+  const lds_f* Wb = Ws_ + 4 * (h * BN + wn0 + l32);
+  f32x4 a[2][T::MR], b[2][T::NR];
+  auto fetch = [&](int tap, int slot) {
+    if (IFD_ABLATE == 2) {
+      asm volatile("" : "+v"(a[slot][0]), "+v"(b[slot][0]));
+      return;
+    }
+    const int toff = (TAPS == 9) ? ((tap / 3) * HWd + (tap % 3)) : 0;
+#pragma unroll
+    for (int mr = 0; mr < T::MR; ++mr) a[slot][mr] = *(const lds_f4*)(Ab + 4 * (pb[mr] + toff));
+#pragma unroll
+    for (int nr = 0; nr < T::NR; ++nr) b[slot][nr] = *(const lds_f4*)(Wb + 4 * (tap * 2 * BN + nr * 32));
+  };
+  fetch(0, 0);
 #pragma unroll
   for (int tap = 0; tap < TAPS; ++tap) {
-    const int toff = (TAPS == 9) ? ((tap / 3) * HWd + (tap % 3)) : 0;
-    f32x4 a[T::MR], b[T::NR];
+    const int cur = tap & 1;
 #pragma unroll
-    for (int mr = 0; mr < T::MR; ++mr) a[mr] = *(const lds_f4*)(As + 4 * (h * NP + pb[mr] + toff));
+    for (int mr = 0; mr < T::MR; ++mr)
 #pragma unroll
-    for (int nr = 0; nr < T::NR; ++nr) b[nr] = *(const lds_f4*)(Ws_ + 4 * ((tap * 2 + h) * BN + wn0 + nr * 32 + l32));
+      for (int nr = 0; nr < T::NR; ++nr)
+        acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][mr][0], b[cur][nr][0], acc[mr][nr], 0, 0, 0);
+    if (tap + 1 < TAPS) fetch(tap + 1, cur ^ 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 1; j < 4; ++j)
 #pragma unroll
       for (int mr = 0; mr < T::MR; ++mr)
 #pragma unroll
         for (int nr = 0; nr < T::NR; ++nr)
-          acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mr][j], b[nr][j], acc[mr][nr], 0, 0, 0);
+          acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][mr][j], b[cur][nr][j], acc[mr][nr], 0, 0, 0);
+    // pin the order: first MFMA group, then the next tap's fragment reads, then the rest
+    __builtin_amdgcn_sched_group_barrier(0x008, T::MR * T::NR, 0);
+    if (tap + 1 < TAPS) __builtin_amdgcn_sched_group_barrier(0x100, T::MR + T::NR, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 3 * T::MR * T::NR, 0);
   }
 }
 
 // One K segment (all chunks of one (source, weights) pair) through the specialised pipeline.
 // Both roles execute exactly 1 + nchunks barriers.
-template <int BN, int WGM, int WGN, int TAPS, int XF>
-__device__ __forceinline__ void run_segment(bool consumer, AccArr<BN, WGM, WGN>& acc, lds_f* smem, int npA,
+template <int BM, int BN, int WGM, int WGN, int TAPS, int XF, int MAXI, bool ONEIMG>
+__device__ __forceinline__ void run_segment(bool consumer, AccArr<BM, BN, WGM, WGN>& acc, lds_f* smem, int npA,
                                             const SegSrc& src, int nchunks, int act, const float* actA,
                                             const float* actB, const float* wbase, int NP, int HHd, int HWd, int n0,
                                             int y0, int x0, int N, int H, int W, int Hs, int Ws,
-                                            const PixArr<BN, WGM, WGN>& pb, int wn0, int k0) {
+                                            const PixArr<BM, BN, WGM, WGN>& pb, int wn0, int k0) {
   lds_f* const A0 = smem;
   lds_f* const A1 = smem + npA * 8;
   lds_f* const W0 = smem + 2 * npA * 8;
@@ -217,43 +261,47 @@ __device__ __forceinline__ void run_segment(bool consumer, AccArr<BN, WGM, WGN>&
   if (consumer) {
     __syncthreads();
     for (int k = 0; k < nchunks; k += 2) {
-      consume<BN, WGM, WGN, TAPS>(acc, A0, W0, NP, HWd, pb, wn0);
+      consume<BM, BN, WGM, WGN, TAPS>(acc, A0, W0, NP, HWd, pb, wn0);
       __syncthreads();
       if (k + 1 >= nchunks) break;
-      consume<BN, WGM, WGN, TAPS>(acc, A1, W1, NP, HWd, pb, wn0);
+      consume<BM, BN, WGM, WGN, TAPS>(acc, A1, W1, NP, HWd, pb, wn0);
       __syncthreads();
     }
   } else {
+    // Producer: two register sets in flight (chunk k+2 loading while chunk k+1 is activated and
+    // written), so each global load has a full consumer period to land.
     const int ptid = threadIdx.x - NP_T;
     const int nitems = (2 * NP + NP_T - 1) / NP_T;
-    using P = Producer<BN, TAPS, XF>;
-    P prod;
-    HaloItem items[MAX_HALO_ITEMS];
-    make_items<TAPS, XF>(items, ptid, NP, HHd, HWd, n0, y0, x0, N, H, W, Hs, Ws);
+    using P = Producer<BN, TAPS, XF, MAXI, ONEIMG>;
+    P pa, pbuf;
+    HaloItem items[MAXI];
+    make_items<TAPS, XF, MAXI>(items, ptid, NP, HHd, HWd, n0, y0, x0, N, H, W, Hs, Ws);
     const int slab = TAPS * 8 * BN;
     const int ctot = src.c0 + src.c1;
-    prod.load(items, nitems, ptid, src, k0, act, actA, actB, ctot, wbase, Ws);
-    prod.store(items, nitems, ptid, act, A0, W0);
+    pa.load(items, nitems, ptid, src, k0, act, actA, actB, ctot, wbase, Ws, n0);
+    if (nchunks > 1) pbuf.load(items, nitems, ptid, src, k0 + 1, act, actA, actB, ctot, wbase + slab, Ws, n0);
+    pa.store(items, nitems, ptid, act, A0, W0);
     __syncthreads();
     for (int k = 0; k < nchunks; k += 2) {
-      if (k + 1 < nchunks) {
-        prod.load(items, nitems, ptid, src, k0 + k + 1, act, actA, actB, ctot, wbase + (size_t)(k + 1) * slab, Ws);
-        prod.store(items, nitems, ptid, act, A1, W1);
-      }
+      if (k + 2 < nchunks)
+        pa.load(items, nitems, ptid, src, k0 + k + 2, act, actA, actB, ctot, wbase + (size_t)(k + 2) * slab, Ws, n0);
+      if (k + 1 < nchunks) pbuf.store(items, nitems, ptid, act, A1, W1);
       __syncthreads();
       if (k + 1 >= nchunks) break;
-      if (k + 2 < nchunks) {
-        prod.load(items, nitems, ptid, src, k0 + k + 2, act, actA, actB, ctot, wbase + (size_t)(k + 2) * slab, Ws);
-        prod.store(items, nitems, ptid, act, A0, W0);
-      }
+      if (k + 3 < nchunks)
+        pbuf.load(items, nitems, ptid, src, k0 + k + 3, act, actA, actB, ctot, wbase + (size_t)(k + 3) * slab, Ws,
+                  n0);
+      if (k + 2 < nchunks) pa.store(items, nitems, ptid, act, A0, W0);
       __syncthreads();
     }
   }
 }
 
-template <int BN, int WGM, int WGN, int TAPS, int XF>
-__global__ __launch_bounds__(NT) void conv_kernel(ConvParams p) {
-  using T = Tile<BN, WGM, WGN>;
+// min 4 waves per SIMD (two 8-wave blocks per CU, <= 128 VGPRs) except the avg-pool variant,
+// whose producer holds 4 source pixels per halo item.
+template <int BM, int BN, int WGM, int WGN, int TAPS, int XF, int MAXI, bool ONEIMG>
+__global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvParams p) {
+  using T = Tile<BM, BN, WGM, WGN>;
   extern __shared__ __attribute__((aligned(16))) float smem_raw[];
   lds_f* const smem = (lds_f*)(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -263,13 +311,21 @@ __global__ __launch_bounds__(NT) void conv_kernel(ConvParams p) {
   const int wm = cw / WGN, wn = cw % WGN;
   const int wm0 = wm * (BM / WGM), wn0 = wn * (BN / WGN);
 
-  int bx = blockIdx.x;
+  // XCD-aware block -> (pixel tile, channel tile) map. Workgroups are dealt round-robin over the
+  // 8 XCDs (blocks b and b+8 share one; MI355X_MICROARCH.md, speed only): the channel tiles of one
+  // pixel tile get IDs 8 apart, so they run on one XCD at about the same time and the second one
+  // reads the activation halo from that XCD's L2 instead of HBM. Bijective on the padded grid.
+  const int nct = p.cout_pad / BN;
+  const int L = blockIdx.x;
+  const int grp = L / (8 * nct), rr = L - grp * 8 * nct;
+  const int ct = rr >> 3;
+  int bx = grp * 8 + (rr & 7);
+  if (bx >= p.npix_tiles) return;  // padding of the last group of 8 (whole block exits: no barrier)
   const int tx = bx % p.tiles_x;
   bx /= p.tiles_x;
   const int ty = bx % p.tiles_y;
   const int tn = bx / p.tiles_y;
   const int n0 = tn * p.IMGS, y0 = ty * p.TH, x0 = tx * p.TW;
-  const int ct = blockIdx.y;
   const int TPI = p.TH * p.TW;  // pixels per image in the tile
 
   constexpr int HALO = (TAPS == 9) ? 1 : 0;
@@ -302,16 +358,18 @@ __global__ __launch_bounds__(NT) void conv_kernel(ConvParams p) {
     const int nch = p.cin_pad / 8;
     const int klo = z * nch / S, khi = (z + 1) * nch / S;
     const float* wbase = p.wpack + ((size_t)ct * nch + klo) * (TAPS * 8 * BN);
-    run_segment<BN, WGM, WGN, TAPS, XF>(consumer, acc, smem, npA, src, khi - klo, p.act, p.actA, p.actB, wbase, NP,
-                                        HHd, HWd, n0, y0, x0, p.N, p.H, p.W, p.Hin, p.Win, pb, wn0, klo);
+    run_segment<BM, BN, WGM, WGN, TAPS, XF, MAXI, ONEIMG>(consumer, acc, smem, npA, src, khi - klo, p.act, p.actA,
+                                                          p.actB, wbase, NP, HHd, HWd, n0, y0, x0, p.N, p.H, p.W,
+                                                          p.Hin, p.Win, pb, wn0, klo);
   }
   // 1x1 segment: ResBlock skip_connection over the raw block input (output resolution)
   if (p.wskip && z == S - 1) {
     SegSrc src{p.s0, p.sc0, p.s1, p.sc1};
     const int nch = p.cs_pad / 8;
     const float* wbase = p.wskip + (size_t)ct * nch * (8 * BN);
-    run_segment<BN, WGM, WGN, 1, XF_NONE>(consumer, acc, smem, npA, src, nch, ACT_NONE, nullptr, nullptr, wbase, BM,
-                                          p.TH, p.TW, n0, y0, x0, p.N, p.H, p.W, p.H, p.W, pm, wn0, 0);
+    run_segment<BM, BN, WGM, WGN, 1, XF_NONE, BM / 128, ONEIMG>(consumer, acc, smem, npA, src, nch, ACT_NONE, nullptr,
+                                                               nullptr, wbase, BM, p.TH, p.TW, n0, y0, x0, p.N, p.H,
+                                                               p.W, p.H, p.W, pm, wn0, 0);
   }
 
   if (p.epi == EPI_NHWC && S > 1) {
@@ -432,47 +490,70 @@ __global__ __launch_bounds__(NT) void conv_kernel(ConvParams p) {
   }
 }
 
-template <int BN, int WGM, int WGN, int TAPS, int XF>
+template <int BM, int BN, int WGM, int WGN, int TAPS, int XF, int MAXI, bool ONEIMG>
+static int launch_inst(const ConvParams& p, size_t lds, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv_kernel<BM, BN, WGM, WGN, TAPS, XF, MAXI, ONEIMG>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  const int ptiles = (p.npix_tiles + 7) / 8 * 8;
+  dim3 grid(ptiles * (p.cout_pad / BN), 1, p.ksplit);
+  hipLaunchKernelGGL((conv_kernel<BM, BN, WGM, WGN, TAPS, XF, MAXI, ONEIMG>), grid, dim3(NT), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WGM, int WGN, int TAPS, int XF>
 static int launch_one(const ConvParams& p, hipStream_t stream) {
   const int HALO = (TAPS == 9) ? 1 : 0;
   const int NP = p.IMGS * (p.TH + 2 * HALO) * (p.TW + 2 * HALO);
   const int npA = NP > BM ? NP : BM;
   const size_t lds = (size_t)(2 * npA * 8 + 2 * 9 * 8 * BN) * sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_kernel<BN, WGM, WGN, TAPS, XF>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
+  const bool one = p.IMGS == 1;
+  if constexpr (BM == 256) {  // only used for W >= 32 (one image per tile, 2*NP <= 1024)
+    if (!one || 2 * NP > 4 * NP_T) return (int)hipErrorInvalidValue;
+    return launch_inst<BM, BN, WGM, WGN, TAPS, XF, 4, true>(p, lds, stream);
+  } else {
+    if (2 * NP <= 2 * NP_T) {
+      if (one) return launch_inst<BM, BN, WGM, WGN, TAPS, XF, 2, true>(p, lds, stream);
+      return launch_inst<BM, BN, WGM, WGN, TAPS, XF, 2, false>(p, lds, stream);
+    }
+    if (2 * NP > 4 * NP_T) return (int)hipErrorInvalidValue;
+    return launch_inst<BM, BN, WGM, WGN, TAPS, XF, 4, false>(p, lds, stream);
   }
-  const int tiles_n = (p.N + p.IMGS - 1) / p.IMGS;
-  dim3 grid(tiles_n * p.tiles_y * p.tiles_x, p.cout_pad / BN, p.ksplit);
-  hipLaunchKernelGGL((conv_kernel<BN, WGM, WGN, TAPS, XF>), grid, dim3(NT), lds, stream, p);
-  return (int)hipGetLastError();
 }
 
-// BN = 64 everywhere it divides Cout: the 49 KB double-buffered LDS footprint admits several
-// blocks per CU, which hides each block's prologue/epilogue behind another's main loop (measured
-// faster than BN = 128 on every UNet layer once the producer/consumer split removed the staging
-// stall). IFD_CONV_BN=128 restores 128-wide tiles for experiments.
 int conv_pick_bn(int cout, int taps, int H, int W, int N) {
   (void)taps; (void)H; (void)W; (void)N;
-  static const char* ov = getenv("IFD_CONV_BN");
-  if (ov && atoi(ov) == 128 && cout % 128 == 0) return 128;
   if (cout % 64 == 0) return 64;
   return 32;
 }
 
+// Tile geometry + split-K. BM = 256 (8 rows x 32 columns of one image) where the layer is wide and
+// the grid still gives >= 2 blocks per CU: it halves the weight-slab loads per MFMA, the producer's
+// bottleneck. Otherwise BM = 128, with split-K to cover the chip on the low-resolution layers.
 void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks) {
+  static const char* ov = getenv("IFD_CONV_BM");  // development override: 128 disables BM=256
+  const bool allow256 = !(ov && atoi(ov) == 128);
+  int bm = 128;
+  if (allow256 && bn == 64 && W >= 32 && H >= 8) {
+    const long blocks256 = (long)N * (H / 8) * (W / 32) * (p.cout_pad / bn);
+    if (blocks256 >= 512) bm = 256;
+  }
+  p.bm = bm;
   p.TW = W < 32 ? W : 32;
-  p.TH = H < BM / p.TW ? H : BM / p.TW;
-  p.IMGS = BM / (p.TH * p.TW);
+  p.TH = H < bm / p.TW ? H : bm / p.TW;
+  p.IMGS = bm / (p.TH * p.TW);
   p.tiles_x = W / p.TW;
   p.tiles_y = H / p.TH;
   p.lg_tw = __builtin_ctz(p.TW);
   p.lg_tpi = __builtin_ctz(p.TH * p.TW);
   const int tiles_n = (N + p.IMGS - 1) / p.IMGS;
-  const long blocks = (long)tiles_n * p.tiles_y * p.tiles_x * (p.cout_pad / bn);
+  p.npix_tiles = tiles_n * p.tiles_y * p.tiles_x;
+  const long blocks = (long)p.npix_tiles * (p.cout_pad / bn);
   // split K until the grid covers ~2 blocks per CU, keeping >= 4 chunks per split
   int S = 1;
   while (S < 8 && blocks * S < 512 && nchunks / (2 * S) >= 4) S *= 2;
@@ -516,19 +597,19 @@ int launch_splitk_reduce(const ConvParams& p, hipStream_t stream) {
 }
 
 int launch_conv(const ConvParams& p, int taps, int xform, int bn, hipStream_t stream) {
-  if (bn == 128) {
-    if (taps == 1) return launch_one<128, 2, 2, 1, XF_NONE>(p, stream);
-    if (xform == XF_NONE) return launch_one<128, 2, 2, 9, XF_NONE>(p, stream);
-    if (xform == XF_UP) return launch_one<128, 2, 2, 9, XF_UP>(p, stream);
-    return launch_one<128, 2, 2, 9, XF_DOWN>(p, stream);
+  if (bn == 64 && p.bm == 256) {
+    if (taps == 1) return (int)hipErrorInvalidValue;
+    if (xform == XF_NONE) return launch_one<256, 64, 4, 1, 9, XF_NONE>(p, stream);
+    if (xform == XF_UP) return launch_one<256, 64, 4, 1, 9, XF_UP>(p, stream);
+    return launch_one<256, 64, 4, 1, 9, XF_DOWN>(p, stream);
   }
   if (bn == 64) {
-    if (taps == 1) return launch_one<64, 2, 2, 1, XF_NONE>(p, stream);
-    if (xform == XF_NONE) return launch_one<64, 2, 2, 9, XF_NONE>(p, stream);
-    if (xform == XF_UP) return launch_one<64, 2, 2, 9, XF_UP>(p, stream);
-    return launch_one<64, 2, 2, 9, XF_DOWN>(p, stream);
+    if (taps == 1) return launch_one<128, 64, 2, 2, 1, XF_NONE>(p, stream);
+    if (xform == XF_NONE) return launch_one<128, 64, 2, 2, 9, XF_NONE>(p, stream);
+    if (xform == XF_UP) return launch_one<128, 64, 2, 2, 9, XF_UP>(p, stream);
+    return launch_one<128, 64, 2, 2, 9, XF_DOWN>(p, stream);
   }
-  if (taps == 9 && xform == XF_NONE) return launch_one<32, 4, 1, 9, XF_NONE>(p, stream);
+  if (taps == 9 && xform == XF_NONE) return launch_one<128, 32, 4, 1, 9, XF_NONE>(p, stream);
   return (int)hipErrorInvalidValue;
 }
 

@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must be loaded first: provides the HIP runtime the library binds to)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libifd.so")
+LIB_PATH = os.environ.get("IFD_LIB_PATH") or os.path.join(_HERE, "libifd.so")  # override: dev ablation builds
 
 c_i64p = ctypes.POINTER(ctypes.c_int64)
 

@@ -239,14 +239,14 @@ def test_script_ddim_full_c1(loops, meta, full_model, name):
     """C1 (256x256, 10-step cosine): the first jump 999->900 divides eps by sqrt(abar_999) = 4.9e-5,
     so the few pixels near the x0 clamp boundary amplify ANY eval rounding difference ~1e4x.
     Bound = the oracle's OWN envelope when its eps is perturbed by a relative 1e-5 (our per-eval
-    deviation from oneDNN is <= ~1e-5 relative; tests/golden/conditioning.py): max-abs within that
-    envelope's max, the fraction of pixels off by > 1e-4 within its fraction, and the 99.9th
-    percentile < 1e-4."""
+    deviation from oneDNN is <= ~1e-5 relative; tests/golden/conditioning.py): max-abs, 99.9th
+    percentile and the fraction of pixels off by > 1e-4 each within that envelope's."""
     import json
     cond = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "conditioning.json")))
     env = [v for k, v in cond.items() if k.startswith(name + "/rel1e-05")]
     env_max = max(v["max"] for v in env)
     env_frac = max(v["frac_gt_1e-4"] for v in env)
+    env_p999 = max(v["p999"] for v in env)
     lm = meta["loops"][name]
     gt, mask = _t(loops[f"{name}/gt"]), _t(loops[f"{name}/mask"])
     y = _run_script_loop(full_model, lm, gt, mask)
@@ -255,4 +255,4 @@ def test_script_ddim_full_c1(loops, meta, full_model, name):
     tol = max(1e-3, env_max)
     print(f"{name}: maxabs={err:.3g} p99.9={p999:.3g} frac>1e-4={frac:.2e} "
           f"(envelope max {env_max:.3g}, frac {env_frac:.2e})")
-    assert err <= tol and p999 < 1e-4 and frac <= max(env_frac, 1e-5)
+    assert err <= tol and p999 <= max(1e-4, env_p999) and frac <= max(env_frac, 1e-5)
