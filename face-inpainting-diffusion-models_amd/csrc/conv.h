@@ -73,6 +73,8 @@ struct ConvParams {
   // sampler epilogue (EPI_DDIM / EPI_DDPM): all NCHW [N,3,H,W] except mask [N,1,H,W]
   float* img; const float* gt; const float* mask; const float* noise; const float* known;
   StepCoeffs sc;
+  // IFD_TRACE builds only: per-block timestamps, 8 x u64 per block (see conv.hip)
+  unsigned long long* trace;
 };
 
 // Launch with the tile configuration chosen from (cout, taps, xform). Returns hipError_t.

@@ -33,6 +33,27 @@
 #ifndef IFD_ABLATE
 #define IFD_ABLATE 0
 #endif
+// IFD_TRACE=1: per-block timestamps (s_memrealtime, 100 MHz) into ConvParams::trace:
+//   [0] entry  [1] consumer past the first barrier  [2] consumer main segment done
+//   [3] consumer epilogue done  [4] producer first chunk written  [5] HW_ID | XCC_ID << 32
+//   [6] producer main segment done  [7] shader cycles entry -> epilogue done (s_memtime)
+#ifndef IFD_TRACE
+#define IFD_TRACE 0
+#endif
+// IFD_PRIO=1: producers at s_setprio 1; =2: consumers at s_setprio 1 (timing experiments)
+#ifndef IFD_PRIO
+#define IFD_PRIO 0
+#endif
+#if IFD_TRACE
+#define TRACE_AT(slot, cond)                                                                     \
+  do {                                                                                           \
+    if (tr && (cond)) tr[slot] = __builtin_amdgcn_s_memrealtime();                               \
+  } while (0)
+#else
+#define TRACE_AT(slot, cond) \
+  do {                       \
+  } while (0)
+#endif
 
 namespace ifd {
 
@@ -253,13 +274,16 @@ __device__ __forceinline__ void run_segment(bool consumer, AccArr<BM, BN, WGM, W
                                             const SegSrc& src, int nchunks, int act, const float* actA,
                                             const float* actB, const float* wbase, int NP, int HHd, int HWd, int n0,
                                             int y0, int x0, int N, int H, int W, int Hs, int Ws,
-                                            const PixArr<BM, BN, WGM, WGN>& pb, int wn0, int k0) {
+                                            const PixArr<BM, BN, WGM, WGN>& pb, int wn0, int k0,
+                                            unsigned long long* tr) {
+  (void)tr;
   lds_f* const A0 = smem;
   lds_f* const A1 = smem + npA * 8;
   lds_f* const W0 = smem + 2 * npA * 8;
   lds_f* const W1 = W0 + 9 * 8 * BN;
   if (consumer) {
     __syncthreads();
+    TRACE_AT(1, threadIdx.x == 0);
     for (int k = 0; k < nchunks; k += 2) {
       consume<BM, BN, WGM, WGN, TAPS>(acc, A0, W0, NP, HWd, pb, wn0);
       __syncthreads();
@@ -281,6 +305,7 @@ __device__ __forceinline__ void run_segment(bool consumer, AccArr<BM, BN, WGM, W
     pa.load(items, nitems, ptid, src, k0, act, actA, actB, ctot, wbase, Ws, n0);
     if (nchunks > 1) pbuf.load(items, nitems, ptid, src, k0 + 1, act, actA, actB, ctot, wbase + slab, Ws, n0);
     pa.store(items, nitems, ptid, act, A0, W0);
+    TRACE_AT(4, ptid == 0);
     __syncthreads();
     for (int k = 0; k < nchunks; k += 2) {
       if (k + 2 < nchunks)
@@ -310,6 +335,8 @@ __global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvPar
   const int cw = wave & 3;
   const int wm = cw / WGN, wn = cw % WGN;
   const int wm0 = wm * (BM / WGM), wn0 = wn * (BN / WGN);
+  if (IFD_PRIO == 1 && !consumer) __builtin_amdgcn_s_setprio(1);
+  if (IFD_PRIO == 2 && consumer) __builtin_amdgcn_s_setprio(1);
 
   // XCD-aware block -> (pixel tile, channel tile) map. Workgroups are dealt round-robin over the
   // 8 XCDs (blocks b and b+8 share one; MI355X_MICROARCH.md, speed only): the channel tiles of one
@@ -327,6 +354,20 @@ __global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvPar
   const int tn = bx / p.tiles_y;
   const int n0 = tn * p.IMGS, y0 = ty * p.TH, x0 = tx * p.TW;
   const int TPI = p.TH * p.TW;  // pixels per image in the tile
+#if IFD_TRACE
+  unsigned long long* const tr =
+      p.trace ? p.trace + 8 * ((size_t)blockIdx.z * gridDim.x + blockIdx.x) : nullptr;
+  const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
+  TRACE_AT(0, tid == 0);
+  if (tr && tid == 0) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    tr[5] = hw | ((unsigned long long)xcc << 32);
+  }
+#else
+  unsigned long long* const tr = nullptr;
+#endif
 
   constexpr int HALO = (TAPS == 9) ? 1 : 0;
   const int HHd = p.TH + 2 * HALO, HWd = p.TW + 2 * HALO;
@@ -360,7 +401,9 @@ __global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvPar
     const float* wbase = p.wpack + ((size_t)ct * nch + klo) * (TAPS * 8 * BN);
     run_segment<BM, BN, WGM, WGN, TAPS, XF, MAXI, ONEIMG>(consumer, acc, smem, npA, src, khi - klo, p.act, p.actA,
                                                           p.actB, wbase, NP, HHd, HWd, n0, y0, x0, p.N, p.H, p.W,
-                                                          p.Hin, p.Win, pb, wn0, klo);
+                                                          p.Hin, p.Win, pb, wn0, klo, tr);
+    TRACE_AT(2, tid == 0);
+    TRACE_AT(6, tid == NP_T);
   }
   // 1x1 segment: ResBlock skip_connection over the raw block input (output resolution)
   if (p.wskip && z == S - 1) {
@@ -369,67 +412,101 @@ __global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvPar
     const float* wbase = p.wskip + (size_t)ct * nch * (8 * BN);
     run_segment<BM, BN, WGM, WGN, 1, XF_NONE, BM / 128, ONEIMG>(consumer, acc, smem, npA, src, nch, ACT_NONE, nullptr,
                                                                nullptr, wbase, BM, p.TH, p.TW, n0, y0, x0, p.N, p.H,
-                                                               p.W, p.H, p.W, pm, wn0, 0);
-  }
-
-  if (p.epi == EPI_NHWC && S > 1) {
-    if (!consumer) return;
-    float* slab = p.part + (size_t)z * p.N * p.H * p.W * p.cout;
-#pragma unroll
-    for (int nr = 0; nr < T::NR; ++nr) {
-      const int co = ct * BN + wn0 + nr * 32 + l32;
-      if (co >= p.cout) continue;
-#pragma unroll
-      for (int mr = 0; mr < T::MR; ++mr)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = wm0 + mr * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int img = m >> p.lg_tpi, rem = m & (TPI - 1);
-          const int n = n0 + img, y = y0 + (rem >> p.lg_tw), x = x0 + (rem & (p.TW - 1));
-          if (n < p.N) gst1(slab + ((size_t)(n * p.H + y) * p.W + x) * p.cout + co, acc[mr][nr][r]);
-        }
-    }
-    return;
+                                                               p.W, p.H, p.W, pm, wn0, 0, nullptr);
   }
 
   if (p.epi == EPI_NHWC) {
-    if (!consumer) return;
+    // Stage the accumulators through LDS, then all 8 waves move 16-byte quads (4 channels of one
+    // pixel): 16 lanes cover one pixel's BN channels. Bias, then residual, in torch's order
+    // (h = conv + bias; out = x_res + h). Split-K writes raw partial sums (splitk_reduce adds the
+    // rest). Residual loads are issued as a batch before any store: on CDNA stores and loads share
+    // vmcnt, so a load issued after a store cannot be waited on without waiting for the store.
+    constexpr int LDE = BN + 4;
+    constexpr int QPP = BN / 4;
+    constexpr int ITEMS = BM * QPP / NT;
+    static_assert(BM * QPP % NT == 0, "epilogue items");
+    lds_f* tile = smem;  // segment buffers are dead after the last barrier
+    const bool split = S > 1;
+    // every item of a thread has the same channel quad (NT % QPP == 0): one bias load, issued
+    // before the LDS round trip so its latency hides behind it
+    const int q = tid % QPP;
+    const int co = ct * BN + 4 * q;
+    const bool co_ok = co < p.cout;
+    f32x4 bias4 = {0.f, 0.f, 0.f, 0.f};
+    if (!split && co_ok) bias4 = gld4(p.bias + co);
+    if (consumer) {
 #pragma unroll
-    for (int nr = 0; nr < T::NR; ++nr) {
-      const int co = ct * BN + wn0 + nr * 32 + l32;
-      if (co >= p.cout) continue;
-      const float bias = gld1(p.bias + co);
+      for (int mr = 0; mr < T::MR; ++mr)
 #pragma unroll
-      for (int mr = 0; mr < T::MR; ++mr) {
+        for (int nr = 0; nr < T::NR; ++nr)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = wm0 + mr * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const int img = m >> p.lg_tpi, rem = m & (TPI - 1);
-          const int py = rem >> p.lg_tw, px = rem & (p.TW - 1);
-          const int n = n0 + img, y = y0 + py, x = x0 + px;
-          if (n >= p.N) continue;
-          float v = acc[mr][nr][r] + bias;
-          if (p.res) {
-            float rv;
-            if (p.res_xform == XF_NONE) {
-              rv = gld1(p.res + ((size_t)(n * p.H + y) * p.W + x) * p.cout + co);
-            } else if (p.res_xform == XF_UP) {
-              rv = gld1(p.res + ((size_t)(n * p.res_H + (y >> 1)) * p.res_W + (x >> 1)) * p.cout + co);
-            } else {
-              const size_t b0 = ((size_t)(n * p.res_H + 2 * y) * p.res_W + 2 * x) * p.cout + co;
-              const size_t rs = (size_t)p.res_W * p.cout;
-              float s = gld1(p.res + b0);
-              s = s + gld1(p.res + b0 + p.cout);
-              s = s + gld1(p.res + b0 + rs);
-              s = s + gld1(p.res + b0 + rs + p.cout);
-              rv = s / 4.0f;
-            }
-            v = rv + v;
+          for (int r = 0; r < 16; ++r) {
+            const int m = wm0 + mr * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            tile[m * LDE + wn0 + nr * 32 + l32] = acc[mr][nr][r];
           }
-          gst1(p.out + ((size_t)(n * p.H + y) * p.W + x) * p.cout + co, v);
+    }
+    __syncthreads();
+    float* const dst = split ? p.part + (size_t)z * p.N * p.H * p.W * p.cout : p.out;
+    f32x4 v[ITEMS];
+    int off[ITEMS];  // float offset within image n (< 2^31: one image's H*W*cout)
+    int nimg[ITEMS];
+    bool ok[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int m = tid / QPP + i * (NT / QPP);
+      const int img = m >> p.lg_tpi, rem = m & (TPI - 1);
+      const int y = y0 + (rem >> p.lg_tw), x = x0 + (rem & (p.TW - 1));
+      nimg[i] = n0 + img;
+      ok[i] = nimg[i] < p.N && co_ok;
+      off[i] = (y * p.W + x) * p.cout + co;
+      v[i] = *(const lds_f4*)(tile + m * LDE + 4 * q);
+      if (!split) v[i] = v[i] + bias4;
+    }
+    if (!split && p.res) {
+      const size_t img_res = (size_t)p.res_H * p.res_W * p.cout;
+      if (p.res_xform == XF_NONE) {
+        f32x4 rv[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+          if (ok[i]) rv[i] = gld4(p.res + nimg[i] * img_res + off[i]);
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+          if (ok[i]) v[i] = rv[i] + v[i];
+      } else {
+        f32x4 rv[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+          if (!ok[i]) continue;
+          const int pix = off[i] / p.cout;
+          const int y = pix / p.W, x = pix - y * p.W;
+          const float* rb = p.res + nimg[i] * img_res + co;
+          if (p.res_xform == XF_UP) {
+            rv[i] = gld4(rb + ((size_t)(y >> 1) * p.res_W + (x >> 1)) * p.cout);
+          } else {
+            const size_t b0 = ((size_t)(2 * y) * p.res_W + 2 * x) * p.cout;
+            const size_t rs = (size_t)p.res_W * p.cout;
+            f32x4 s = gld4(rb + b0);
+            s = s + gld4(rb + b0 + p.cout);
+            s = s + gld4(rb + b0 + rs);
+            s = s + gld4(rb + b0 + rs + p.cout);
+            rv[i] = s / 4.0f;
+          }
         }
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+          if (ok[i]) v[i] = rv[i] + v[i];
       }
     }
+    const size_t img_out = (size_t)p.H * p.W * p.cout;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i)
+      if (ok[i]) *(__attribute__((address_space(1))) f32x4*)(dst + nimg[i] * img_out + off[i]) = v[i];
+#if IFD_TRACE
+    if (tr && tid == 0) {
+      tr[3] = __builtin_amdgcn_s_memrealtime();
+      tr[7] = __builtin_amdgcn_s_memtime() - cyc0;
+    }
+#endif
     return;
   }
 
@@ -511,7 +588,11 @@ static int launch_one(const ConvParams& p, hipStream_t stream) {
   const int HALO = (TAPS == 9) ? 1 : 0;
   const int NP = p.IMGS * (p.TH + 2 * HALO) * (p.TW + 2 * HALO);
   const int npA = NP > BM ? NP : BM;
-  const size_t lds = (size_t)(2 * npA * 8 + 2 * 9 * 8 * BN) * sizeof(float);
+  const size_t stage = (size_t)(2 * npA * 8 + 2 * 9 * 8 * BN);
+  const size_t epi = (size_t)BM * (BN + 4);  // NHWC epilogue tile (the final-conv tile is smaller)
+  static const char* pad_env = getenv("IFD_CONV_LDS_PAD");  // development: force 1 block / CU
+  const size_t pad = pad_env ? (size_t)atoi(pad_env) : 0;
+  const size_t lds = (stage > epi ? stage : epi) * sizeof(float) + pad;
   const bool one = p.IMGS == 1;
   if constexpr (BM == 256) {  // only used for W >= 32 (one image per tile, 2*NP <= 1024)
     if (!one || 2 * NP > 4 * NP_T) return (int)hipErrorInvalidValue;

@@ -11,6 +11,7 @@
 #include <array>
 #include <cstdio>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace ifd {
@@ -496,9 +497,51 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   p.img = img; p.gt = gt; p.mask = mask; p.noise = noise; p.known = known;
   IFD_REQUIRE(c0 % 8 == 0 && c1 % 8 == 0 && c0 + c1 == cw.cin_pad, "conv input channels");
   IFD_REQUIRE(!cw.has_skip || (sc0 + sc1 == cw.cs_pad && sc0 % 8 == 0 && sc1 % 8 == 0), "skip channels");
+#if IFD_TRACE
+  // development builds: dump per-block timestamps of the IFD_TRACE_NTH launch whose layer name
+  // contains IFD_TRACE_MATCH into IFD_TRACE_FILE (+ ".json" with the geometry)
+  const char* tmatch = getenv("IFD_TRACE_MATCH");  // read per call: a driver may set it mid-run
+  const int tnth = getenv("IFD_TRACE_NTH") ? atoi(getenv("IFD_TRACE_NTH")) : 0;
+  static int tseen = 0;
+  static std::string tlast;
+  if (tmatch && tlast != tmatch) {
+    tlast = tmatch;
+    tseen = 0;
+  }
+  unsigned long long* tbuf = nullptr;
+  size_t tblocks = 0;
+  char tname[160];
+  snprintf(tname, sizeof(tname), "r%d %d+%d->%d skip%d xf%d", H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0, xf);
+  if (tmatch && strstr(tname, tmatch) && tseen++ == tnth) {
+    tblocks = (size_t)((p.npix_tiles + 7) / 8 * 8) * (cw.cout_pad / cw.bn) * p.ksplit;
+    IFD_CHECK_HIP(hipMalloc(&tbuf, tblocks * 8 * sizeof(unsigned long long)));
+    IFD_CHECK_HIP(hipMemsetAsync(tbuf, 0, tblocks * 8 * sizeof(unsigned long long), s));
+    p.trace = tbuf;
+  }
+#endif
   hipEvent_t e0;
   prof_begin(s, &e0);
   int e = launch_conv(p, cw.taps, xf, cw.bn, s);
+#if IFD_TRACE
+  if (tbuf) {
+    IFD_CHECK_HIP(hipStreamSynchronize(s));
+    std::vector<unsigned long long> hbuf(tblocks * 8);
+    IFD_CHECK_HIP(hipMemcpy(hbuf.data(), tbuf, hbuf.size() * 8, hipMemcpyDeviceToHost));
+    IFD_CHECK_HIP(hipFree(tbuf));
+    const char* fn = getenv("IFD_TRACE_FILE") ? getenv("IFD_TRACE_FILE") : "conv_trace.bin";
+    if (FILE* f = fopen(fn, "wb")) {
+      fwrite(hbuf.data(), 8, hbuf.size(), f);
+      fclose(f);
+    }
+    std::string jn = std::string(fn) + ".json";
+    if (FILE* f = fopen(jn.c_str(), "w")) {
+      fprintf(f, "{\"layer\": \"%s\", \"blocks\": %zu, \"bm\": %d, \"bn\": %d, \"npix_tiles\": %d, "
+                 "\"ksplit\": %d, \"nct\": %d, \"chunks\": %d}\n",
+              tname, tblocks, p.bm, cw.bn, p.npix_tiles, p.ksplit, cw.cout_pad / cw.bn, cw.cin_pad / 8);
+      fclose(f);
+    }
+  }
+#endif
   if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, s);
   if (prof_on_) {
     // algorithmic work: 2*MAC over real channels; bytes = activations in + weights + out (once each)
@@ -509,10 +552,11 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                                 (cw.has_skip ? pix * cw.cs : 0) + (res ? pix * cw.cout : 0));
     char nm[160];
     if (prof_layers_)
-      snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%d> r%d %d+%d->%d skip%d", cw.bn, cw.taps, xf, H, c0, c1, cw.cout,
-               cw.has_skip ? cw.cs : 0);
-    else
-      snprintf(nm, sizeof(nm), "conv_kernel<%d,%s,%d,%d>", cw.bn, cw.bn == 32 ? "4,1" : "2,2", cw.taps, xf);
+      snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%d,%d> r%d %d+%d->%d skip%d", p.bm, cw.bn, cw.taps, xf, H, c0, c1,
+               cw.cout, cw.has_skip ? cw.cs : 0);
+    else  // same template arguments (BM,BN,WGM,WGN,TAPS,XF) as the rocprof kernel name
+      snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%s,%d,%d>", p.bm, cw.bn,
+               (p.bm == 256 || cw.bn == 32) ? "4,1" : "2,2", cw.taps, xf);
     prof_end(s, e0, nm, flops, bytes);
   }
   if (e) {
