@@ -24,16 +24,12 @@
 // 9*8*BN floats per chunk, reused by BM pixels) is what BM = 256 amortises.
 // fp32 in / fp32 accumulate: the MFMA result is an exact fp32 fma chain (no reduced precision).
 #include "conv.h"
+#include "conv_dev.h"
 
 #include <cstdlib>
 
-// Timing-only ablation builds (never shipped; outputs are garbage):
-//   IFD_ABLATE=1  producers skip every load / store (barriers only)
-//   IFD_ABLATE=2  consumers skip the fragment ds_reads (MFMAs on stale registers)
-#ifndef IFD_ABLATE
-#define IFD_ABLATE 0
-#endif
-// IFD_TRACE=1: per-block timestamps (s_memrealtime, 100 MHz) into ConvParams::trace:
+// IFD_ABLATE (timing-only ablation builds): see conv_dev.h.
+// IFD_TRACE=1: per-block timestamps (s_memrealtime, 100 MHz) into ConvParams::trace (64 slots/block):
 //   [0] entry  [1] consumer past the first barrier  [2] consumer main segment done
 //   [3] consumer epilogue done  [4] producer first chunk written  [5] HW_ID | XCC_ID << 32
 //   [6] producer main segment done  [7] shader cycles entry -> epilogue done (s_memtime)
@@ -57,39 +53,6 @@
 
 namespace ifd {
 
-// Explicit address spaces: without them the LDS / global accesses compile to flat_* ops, which
-// count on BOTH vmcnt and lgkmcnt, so an LDS-read wait would also wait for in-flight global loads.
-typedef __attribute__((address_space(3))) float lds_f;
-typedef __attribute__((address_space(3))) f32x4 lds_f4;
-typedef __attribute__((address_space(1))) const f32x4 glb_f4;
-typedef __attribute__((address_space(1))) const float glb_f;
-
-__device__ __forceinline__ f32x4 gld4(const float* p) { return *(glb_f4*)(p); }
-__device__ __forceinline__ float gld1(const float* p) { return *(glb_f*)(p); }
-__device__ __forceinline__ void gst1(float* p, float v) { *(__attribute__((address_space(1))) float*)(p) = v; }
-
-constexpr int NT = 512;    // threads per block
-constexpr int NP_T = 256;  // producer threads (waves 4-7)
-
-// SiLU of the GroupNorm-applied value: x * rcp(1 + 2^(-x*log2 e)) on v_exp_f32 / v_rcp_f32
-// (relative error < 1e-6 for |x| < 10 against torch's x / (1 + exp(-x)); a whole UNet eval stays
-// at ~2e-6 max-abs from the reference). The producer waves bound the pipeline, so the short form.
-__device__ __forceinline__ float silu_fast(float x) {
-  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
-}
-
-template <int BM, int BN, int WGM, int WGN>
-struct Tile {
-  static constexpr int MR = BM / WGM / 32;
-  static constexpr int NR = BN / WGN / 32;
-  static_assert(MR >= 1 && NR >= 1, "bad wave grid");
-  static_assert(WGM * WGN == 4, "4 consumer waves");
-};
-
-template <int BM, int BN, int WGM, int WGN>
-using AccArr = f32x16[Tile<BM, BN, WGM, WGN>::MR][Tile<BM, BN, WGM, WGN>::NR];
-template <int BM, int BN, int WGM, int WGN>
-using PixArr = int[Tile<BM, BN, WGM, WGN>::MR];
 
 struct SegSrc {
   const float* p0; int c0;
@@ -222,51 +185,6 @@ struct Producer {
   }
 };
 
-// MFMAs over one staged chunk (consumer waves). Fragment reads are software-pipelined one tap
-// ahead (two register slots, fully unrolled so the slots are static).
-template <int BM, int BN, int WGM, int WGN, int TAPS>
-__device__ __forceinline__ void consume(AccArr<BM, BN, WGM, WGN>& acc, const lds_f* As, const lds_f* Ws_, int NP,
-                                        int HWd, const PixArr<BM, BN, WGM, WGN>& pb, int wn0) {
-  using T = Tile<BM, BN, WGM, WGN>;
-  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-  const lds_f* Ab = As + 4 * h * NP;
-  const lds_f* Wb = Ws_ + 4 * (h * BN + wn0 + l32);
-  f32x4 a[2][T::MR], b[2][T::NR];
-  auto fetch = [&](int tap, int slot) {
-    if (IFD_ABLATE == 2) {
-      asm volatile("" : "+v"(a[slot][0]), "+v"(b[slot][0]));
-      return;
-    }
-    const int toff = (TAPS == 9) ? ((tap / 3) * HWd + (tap % 3)) : 0;
-#pragma unroll
-    for (int mr = 0; mr < T::MR; ++mr) a[slot][mr] = *(const lds_f4*)(Ab + 4 * (pb[mr] + toff));
-#pragma unroll
-    for (int nr = 0; nr < T::NR; ++nr) b[slot][nr] = *(const lds_f4*)(Wb + 4 * (tap * 2 * BN + nr * 32));
-  };
-  fetch(0, 0);
-#pragma unroll
-  for (int tap = 0; tap < TAPS; ++tap) {
-    const int cur = tap & 1;
-#pragma unroll
-    for (int mr = 0; mr < T::MR; ++mr)
-#pragma unroll
-      for (int nr = 0; nr < T::NR; ++nr)
-        acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][mr][0], b[cur][nr][0], acc[mr][nr], 0, 0, 0);
-    if (tap + 1 < TAPS) fetch(tap + 1, cur ^ 1);
-#pragma unroll
-    for (int j = 1; j < 4; ++j)
-#pragma unroll
-      for (int mr = 0; mr < T::MR; ++mr)
-#pragma unroll
-        for (int nr = 0; nr < T::NR; ++nr)
-          acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[cur][mr][j], b[cur][nr][j], acc[mr][nr], 0, 0, 0);
-    // pin the order: first MFMA group, then the next tap's fragment reads, then the rest
-    __builtin_amdgcn_sched_group_barrier(0x008, T::MR * T::NR, 0);
-    if (tap + 1 < TAPS) __builtin_amdgcn_sched_group_barrier(0x100, T::MR + T::NR, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 3 * T::MR * T::NR, 0);
-  }
-}
-
 // One K segment (all chunks of one (source, weights) pair) through the specialised pipeline.
 // Both roles execute exactly 1 + nchunks barriers.
 template <int BM, int BN, int WGM, int WGN, int TAPS, int XF, int MAXI, bool ONEIMG>
@@ -356,7 +274,7 @@ __global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvPar
   const int TPI = p.TH * p.TW;  // pixels per image in the tile
 #if IFD_TRACE
   unsigned long long* const tr =
-      p.trace ? p.trace + 8 * ((size_t)blockIdx.z * gridDim.x + blockIdx.x) : nullptr;
+      p.trace ? p.trace + 64 * ((size_t)blockIdx.z * gridDim.x + blockIdx.x) : nullptr;
   const unsigned long long cyc0 = __builtin_amdgcn_s_memtime();
   TRACE_AT(0, tid == 0);
   if (tr && tid == 0) {

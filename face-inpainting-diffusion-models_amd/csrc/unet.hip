@@ -514,18 +514,20 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   snprintf(tname, sizeof(tname), "r%d %d+%d->%d skip%d xf%d", H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0, xf);
   if (tmatch && strstr(tname, tmatch) && tseen++ == tnth) {
     tblocks = (size_t)((p.npix_tiles + 7) / 8 * 8) * (cw.cout_pad / cw.bn) * p.ksplit;
-    IFD_CHECK_HIP(hipMalloc(&tbuf, tblocks * 8 * sizeof(unsigned long long)));
-    IFD_CHECK_HIP(hipMemsetAsync(tbuf, 0, tblocks * 8 * sizeof(unsigned long long), s));
+    IFD_CHECK_HIP(hipMalloc(&tbuf, tblocks * 64 * sizeof(unsigned long long)));
+    IFD_CHECK_HIP(hipMemsetAsync(tbuf, 0, tblocks * 64 * sizeof(unsigned long long), s));
     p.trace = tbuf;
   }
 #endif
   hipEvent_t e0;
   prof_begin(s, &e0);
-  int e = launch_conv(p, cw.taps, xf, cw.bn, s);
+  const char* st_env = getenv("IFD_CONV_STREAM");  // development switch (default on)
+  const bool use_stream = !(st_env && st_env[0] == '0') && conv_stream_eligible(p, cw.taps, xf, cw.bn);
+  int e = use_stream ? launch_conv_stream(p, xf, s) : launch_conv(p, cw.taps, xf, cw.bn, s);
 #if IFD_TRACE
   if (tbuf) {
     IFD_CHECK_HIP(hipStreamSynchronize(s));
-    std::vector<unsigned long long> hbuf(tblocks * 8);
+    std::vector<unsigned long long> hbuf(tblocks * 64);
     IFD_CHECK_HIP(hipMemcpy(hbuf.data(), tbuf, hbuf.size() * 8, hipMemcpyDeviceToHost));
     IFD_CHECK_HIP(hipFree(tbuf));
     const char* fn = getenv("IFD_TRACE_FILE") ? getenv("IFD_TRACE_FILE") : "conv_trace.bin";
@@ -536,8 +538,8 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     std::string jn = std::string(fn) + ".json";
     if (FILE* f = fopen(jn.c_str(), "w")) {
       fprintf(f, "{\"layer\": \"%s\", \"blocks\": %zu, \"bm\": %d, \"bn\": %d, \"npix_tiles\": %d, "
-                 "\"ksplit\": %d, \"nct\": %d, \"chunks\": %d}\n",
-              tname, tblocks, p.bm, cw.bn, p.npix_tiles, p.ksplit, cw.cout_pad / cw.bn, cw.cin_pad / 8);
+                 "\"ksplit\": %d, \"nct\": %d, \"chunks\": %d, \"stream\": %d}\n",
+              tname, tblocks, p.bm, cw.bn, p.npix_tiles, p.ksplit, cw.cout_pad / cw.bn, cw.cin_pad / 8, (int)use_stream);
       fclose(f);
     }
   }

@@ -94,6 +94,31 @@ def test_unet_batch_independent(evals, red_model):
             assert torch.equal(y1, yb[i:i + 1]), i
 
 
+def test_stream_conv_bitwise(full_model):
+    """The persistent streaming conv (wide layers) and the one-tile-per-block conv sum in the same
+    order: outputs must be bit-identical. B=3 256x256 also exercises a tile count that is not a
+    multiple of the grid."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(3, 3, 256, 256, device=DEV, generator=g)
+    gt = torch.rand(3, 3, 256, 256, device=DEV, generator=g) * 2 - 1
+    mask = (torch.rand(3, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
+    t = torch.tensor([999, 500, 3], device=DEV)
+    old = os.environ.get("IFD_CONV_STREAM")
+    try:
+        with torch.no_grad():
+            os.environ["IFD_CONV_STREAM"] = "1"
+            y1 = full_model(x, t, masked_image=gt * (1 - mask), mask=mask).clone()
+            os.environ["IFD_CONV_STREAM"] = "0"
+            y0 = full_model(x, t, masked_image=gt * (1 - mask), mask=mask).clone()
+    finally:
+        if old is None:
+            os.environ.pop("IFD_CONV_STREAM", None)
+        else:
+            os.environ["IFD_CONV_STREAM"] = old
+    assert torch.isfinite(y1).all()
+    assert torch.equal(y0, y1), maxabs(y0, y1)
+
+
 def _step_inputs(B=2, H=64, seed=0):
     g = torch.Generator().manual_seed(seed)
     out6 = torch.randn(B, 6, H, H, generator=g)

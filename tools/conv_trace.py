@@ -25,9 +25,30 @@ from ifd.topology import FULL  # noqa: E402
 TICK_NS = 10.0  # s_memrealtime: 100 MHz
 
 
+def analyze_stream(meta, a):
+    """conv_stream records: s_memtime stamps of intervals 8..15 (see conv_stream.hip)."""
+    a = a[a[:, 63] != 0]
+    st = a[:, :64].reshape(len(a), 8, 8)[:, :, :7].astype(np.float64)  # [block, interval, slot]
+    P0, P1, P2, P3, C0, C1, P6 = (st[:, :, i] for i in range(7))
+
+    def q(v):
+        v = np.asarray(v).ravel()
+        return {"p10": round(float(np.percentile(v, 10))), "p50": round(float(np.median(v))),
+                "p90": round(float(np.percentile(v, 90)))}
+    return {"meta": meta, "blocks": int(len(a)), "units": "shader cycles",
+            "interval (consumer start->start)": q(C0[:, 1:] - C0[:, :-1]),
+            "consumer MFMA issue": q(C1 - C0), "consumer wait at barrier": q(C0[:, 1:] - C1[:, :-1]),
+            "producer drain (old loads)": q(P6 - P0), "producer load issue after drain": q(P1 - P6), "producer store (incl. vmcnt waits)": q(P2 - P1),
+            "producer epilogue": q(P3 - P2), "producer wait at barrier": q(P0[:, 1:] - P3[:, :-1]),
+            "producer busy": q(P3 - P0)}
+
+
 def analyze(fn):
     meta = json.load(open(fn + ".json"))
-    a = np.fromfile(fn, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    a = np.fromfile(fn, dtype=np.uint64).reshape(-1, 64).astype(np.int64)
+    if meta.get("stream"):
+        return analyze_stream(meta, a)
+    a = a[:, :8]
     live = a[:, 0] > 0
     a = a[live]
     t0 = a[:, 0].min()
