@@ -85,7 +85,7 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks);
 int launch_splitk_reduce(const ConvParams& p, hipStream_t stream);
 // Persistent streaming kernel for the wide layers (conv_stream.hip).
 bool conv_stream_eligible(const ConvParams& p, int taps, int xform, int bn);
-int launch_conv_stream(const ConvParams& p, int xform, hipStream_t stream);
+int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t stream);
 
 // Shared elementwise step math, also used by the standalone step kernels (sampler.hip).
 __device__ __forceinline__ float ddim_step_value(const StepCoeffs& s, float img, float eps, float noise,

@@ -459,6 +459,146 @@ __global__ __launch_bounds__(64 * CW + NP_T, CW == 4 ? 2 : 3) void conv_stream_k
   TRACE_FLUSH(PT0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Mode 2: TWO persistent workgroups per CU (<= 80 KiB LDS each). The two pipelines on a CU are
+// independent, so one workgroup's latency tails (producer load waits, the epilogue) overlap the
+// other's MFMAs — what the one-tile-per-workgroup kernel gets from two co-resident blocks —
+// while the chunk stream still runs across tiles without a fill. LDS: A stages (2 x 10.6 KiB),
+// W ring of 2 slots (weights of chunk j+1 DMA'd during interval j, 2 x 20 KiB), and a 4.25 KiB
+// staging strip per consumer wave for the epilogue, which the consumers do themselves.
+constexpr int S2_STRIP = 16 * SLDE;                          // 16 pixels x 68 floats
+constexpr int S2_LDS_FLOATS = 2 * SA + 2 * SWP + 4 * S2_STRIP;  // 19952 floats = 77.9 KiB
+
+template <int XF>
+__global__ __launch_bounds__(NT, 4) void conv_stream2_kernel(ConvParams p) {
+  using T = Tile<SBM, SBN, 4, 1>;
+  extern __shared__ __attribute__((aligned(16))) float smem_raw[];
+  lds_f* const smem = (lds_f*)(smem_raw);
+  lds_f* const A0 = smem;
+  lds_f* const W0 = smem + 2 * SA;  // slot c & 1 at W0 + (c & 1) * SWP
+  lds_f* const ST = smem + 2 * SA + 2 * SWP;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool consumer = __builtin_amdgcn_readfirstlane(wave) < 4;
+  const int nct = p.cout_pad / SBN;
+  const int nvirt = p.npix_tiles * nct;
+  const int G = gridDim.x;
+  const int ntile = (nvirt - (int)blockIdx.x + G - 1) / G;  // host guarantees >= 1
+  const int nch = p.cin_pad / 8;
+  const int J = ntile * nch;
+  auto tile_of = [&](int ti) { return decode_tile(p, (int)blockIdx.x + ti * G, nct); };
+
+  if (consumer) {
+    const int h = lane >> 5, l32 = lane & 31;
+    const int wm0 = wave * (SBM / 4);
+    lds_f* const strip = ST + wave * S2_STRIP;
+    f32x16 acc[T::MR][T::NR];
+    int pb[T::MR];
+#pragma unroll
+    for (int mr = 0; mr < T::MR; ++mr) {
+      const int m = wm0 + mr * 32 + l32;
+      pb[mr] = (m >> 5) * SHW + (m & 31);
+    }
+    auto zero = [&]() {
+#pragma unroll
+      for (int mr = 0; mr < T::MR; ++mr)
+#pragma unroll
+        for (int nr = 0; nr < T::NR; ++nr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[mr][nr][r] = 0.f;
+    };
+    // epilogue lane map: channel quad q = lane & 15 of piece pixels (lane >> 4) + 4 v
+    const int q = lane & 15, prow = lane >> 4;
+    // Wave-private epilogue of one tile: 4 pieces of 16 pixels (half of one 32-pixel MFMA row
+    // block each) through the strip; bias then residual (torch order), 16-byte stores.
+    auto epilogue = [&](const STile& t) {
+      const rsrc_t ro = mkrsrc(p.out + (size_t)t.n0 * p.H * p.W * p.cout);
+      const rsrc_t rr = mkrsrc(p.res ? p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout : p.out);
+      const int co = t.ct * SBN + 4 * q;
+      const f32x4 bias4 = gld4(p.bias + co);
+#pragma unroll
+      for (int piece = 0; piece < 2 * T::MR; ++piece) {
+        const int mr = piece >> 1, half = piece & 1;
+        int goff[4];
+        f32x4 rv[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int m = wm0 + 32 * mr + 16 * half + prow + 4 * v;
+          const int y = t.y0 + (m >> 5), x = t.x0 + (m & 31);
+          goff[v] = ((y * p.W + x) * p.cout + co) * 4;
+          if (p.res) {
+            const int ro_ = p.res_xform == XF_NONE ? goff[v]
+                                                   : (((y >> 1) * p.res_W + (x >> 1)) * p.cout + co) * 4;
+            rv[v] = bld4(rr, ro_, 0);
+          }
+        }
+#pragma unroll
+        for (int nr = 0; nr < T::NR; ++nr)
+#pragma unroll
+          for (int rr8 = 0; rr8 < 8; ++rr8) {
+            const int r = 8 * half + rr8;
+            const int pp = (r & 3) + 8 * ((r >> 2) & 1) + 4 * h;  // pixel within the piece
+            strip[pp * SLDE + nr * 32 + l32] = acc[mr][nr][r];
+          }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          f32x4 val = *(const lds_f4*)(strip + (prow + 4 * v) * SLDE + 4 * q);
+          val = val + bias4;
+          if (p.res) val = rv[v] + val;
+          bst4(ro, goff[v], val);
+        }
+      }
+    };
+    zero();
+    BARRIER_CONSUMER();  // chunk 0 staged
+    int k = 0, ti = 0;
+    for (int j = 0; j < J; ++j) {
+      consume<SBM, SBN, 4, 1, 9>(acc, A0 + (j & 1) * SA, W0 + (j & 1) * SWP, SNP, SHW, pb, 0);
+      if (++k == nch) {
+        k = 0;
+        epilogue(tile_of(ti++));
+        zero();
+      }
+      BARRIER_CONSUMER();
+    }
+    return;
+  }
+
+  // ---- producers: halo two chunks ahead in registers, weights one chunk ahead by LDS-DMA ----
+  const int ptid = tid - NP_T;
+  SProducer<XF> P;
+  P.init(ptid);
+  SSet<XF> s0, s1;
+  auto load_chunk = [&](SSet<XF>& s, int c) {
+    c = min(c, J - 1);
+    const int ti = c / nch, kk = c - ti * nch;
+    P.load(s, p, tile_of(ti), ti, kk, nch);
+  };
+  auto dma_chunk = [&](int c) {
+    c = min(c, J - 1);
+    const int ti = c / nch, kk = c - ti * nch;
+    P.dma_weights(p, tile_of(ti).ct, kk, nch, W0 + (c & 1) * SWP);
+  };
+  dma_chunk(0);
+  load_chunk(s0, 0);
+  load_chunk(s1, 1);
+  P.store(s0, p.act, A0);
+  BARRIER_PRODUCER(5);  // chunk 0's weights landed (younger: chunk 1's five halo/coef loads)
+  // interval j: weights of chunk j+1 (DMA, first so a vmcnt can single them out), halo of chunk
+  // j+2, LDS writes of chunk j+1, barrier once the DMA has landed
+  for (int j = 0; j < J; j += 2) {
+    dma_chunk(j + 1);
+    load_chunk(s0, j + 2);
+    if (j + 1 < J) P.store(s1, p.act, A0 + SA);
+    BARRIER_PRODUCER(5);
+    if (j + 1 >= J) break;
+    dma_chunk(j + 2);
+    load_chunk(s1, j + 3);
+    if (j + 2 < J) P.store(s0, p.act, A0);
+    BARRIER_PRODUCER(5);
+  }
+}
+
 }  // namespace
 
 size_t conv_stream_lds_bytes() { return (size_t)SLDS_FLOATS * sizeof(float) + (IFD_TRACE ? 512 : 0); }
@@ -497,7 +637,35 @@ static int launch_stream_inst(const ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-int launch_conv_stream(const ConvParams& p, int xform, hipStream_t stream) {
+template <int XF>
+static int launch_stream2_inst(const ConvParams& p, hipStream_t stream) {
+  static bool attr_set = false;
+  const size_t lds = (size_t)S2_LDS_FLOATS * sizeof(float);
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_stream2_kernel<XF>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const int nvirt = p.npix_tiles * (p.cout_pad / SBN);
+  const int grid = nvirt < 2 * ncu ? nvirt : 2 * ncu;  // two workgroups per CU
+  hipLaunchKernelGGL((conv_stream2_kernel<XF>), dim3(grid), dim3(NT), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
+int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t stream) {
+  if (mode == 2) {
+    if (xform == XF_NONE) return launch_stream2_inst<XF_NONE>(p, stream);
+    if (xform == XF_UP) return launch_stream2_inst<XF_UP>(p, stream);
+    return (int)hipErrorInvalidValue;
+  }
   const char* cw_env = getenv("IFD_STREAM_CW");  // development: 4 or 8 consumer waves
   const bool cw4 = cw_env && atoi(cw_env) == 4;
   if (xform == XF_NONE) return cw4 ? launch_stream_inst<XF_NONE, 4>(p, stream) : launch_stream_inst<XF_NONE, 8>(p, stream);

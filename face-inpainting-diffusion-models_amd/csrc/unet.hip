@@ -16,6 +16,8 @@
 
 namespace ifd {
 
+constexpr int kDefaultStreamMode = 2;
+
 static int ceil_to(int v, int m) { return (v + m - 1) / m * m; }
 
 Model::Model(const ifd_config& cfg) : cfg_(cfg) { build_plan(); }
@@ -521,9 +523,12 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
 #endif
   hipEvent_t e0;
   prof_begin(s, &e0);
-  const char* st_env = getenv("IFD_CONV_STREAM");  // development switch (default on)
-  const bool use_stream = !(st_env && st_env[0] == '0') && conv_stream_eligible(p, cw.taps, xf, cw.bn);
-  int e = use_stream ? launch_conv_stream(p, xf, s) : launch_conv(p, cw.taps, xf, cw.bn, s);
+  // IFD_CONV_STREAM selects the wide-layer kernel: 0 one tile per workgroup (conv.hip), 1 one
+  // persistent workgroup per CU, 2 two persistent workgroups per CU (conv_stream.hip)
+  const char* st_env = getenv("IFD_CONV_STREAM");
+  const int stream_mode = st_env ? atoi(st_env) : kDefaultStreamMode;
+  const bool use_stream = stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn);
+  int e = use_stream ? launch_conv_stream(p, xf, stream_mode, s) : launch_conv(p, cw.taps, xf, cw.bn, s);
 #if IFD_TRACE
   if (tbuf) {
     IFD_CHECK_HIP(hipStreamSynchronize(s));
@@ -554,9 +559,13 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                                 (cw.has_skip ? pix * cw.cs : 0) + (res ? pix * cw.cout : 0));
     char nm[160];
     if (prof_layers_)
-      snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%d,%d> r%d %d+%d->%d skip%d", p.bm, cw.bn, cw.taps, xf, H, c0, c1,
-               cw.cout, cw.has_skip ? cw.cs : 0);
-    else  // same template arguments (BM,BN,WGM,WGN,TAPS,XF) as the rocprof kernel name
+      snprintf(nm, sizeof(nm), "%s<%d,%d,%d,%d> r%d %d+%d->%d skip%d", use_stream ? "conv_stream" : "conv_kernel", p.bm,
+               cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
+    else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
+      snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
+    else if (use_stream)
+      snprintf(nm, sizeof(nm), "conv_stream_kernel<%d,%d>", xf, getenv("IFD_STREAM_CW") ? atoi(getenv("IFD_STREAM_CW")) : 8);
+    else  // (BM,BN,WGM,WGN,TAPS,XF)
       snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%s,%d,%d>", p.bm, cw.bn,
                (p.bm == 256 || cw.bn == 32) ? "4,1" : "2,2", cw.taps, xf);
     prof_end(s, e0, nm, flops, bytes);

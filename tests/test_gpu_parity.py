@@ -94,10 +94,11 @@ def test_unet_batch_independent(evals, red_model):
             assert torch.equal(y1, yb[i:i + 1]), i
 
 
-def test_stream_conv_bitwise(full_model):
-    """The persistent streaming conv (wide layers) and the one-tile-per-block conv sum in the same
-    order: outputs must be bit-identical. B=3 256x256 also exercises a tile count that is not a
-    multiple of the grid."""
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_stream_conv_bitwise(full_model, mode):
+    """The persistent streaming convs (wide layers; mode 1: one workgroup per CU, mode 2: two)
+    and the one-tile-per-workgroup conv sum in the same order: outputs must be bit-identical.
+    B=3 256x256 also exercises tile counts that are not multiples of the grid."""
     g = torch.Generator(device=DEV).manual_seed(3)
     x = torch.randn(3, 3, 256, 256, device=DEV, generator=g)
     gt = torch.rand(3, 3, 256, 256, device=DEV, generator=g) * 2 - 1
@@ -106,7 +107,7 @@ def test_stream_conv_bitwise(full_model):
     old = os.environ.get("IFD_CONV_STREAM")
     try:
         with torch.no_grad():
-            os.environ["IFD_CONV_STREAM"] = "1"
+            os.environ["IFD_CONV_STREAM"] = mode
             y1 = full_model(x, t, masked_image=gt * (1 - mask), mask=mask).clone()
             os.environ["IFD_CONV_STREAM"] = "0"
             y0 = full_model(x, t, masked_image=gt * (1 - mask), mask=mask).clone()

@@ -11,10 +11,11 @@ bench = json.load(open(os.path.join(g, f"bench_{tag}.json")))
 shutil.copy(os.path.join(g, f"bench_{tag}.json"), os.path.join(out, "bench.json"))
 shutil.copy(os.path.join(g, f"prof_{tag}", "trace_kernel_stats.csv"), os.path.join(out, "rocprof_kernel_stats.csv"))
 rf = bench["roofline"]
-dom = rf["kernel"]  # e.g. conv_kernel<64,2,2,9,0>
-inst = dom[len("conv_kernel<"):-1].split(",")
-# rocprof names: "void ifd::conv_kernel<64, 2, 2, 9, 0, 2>(ifd::ConvParams)" (extra MAXI arg possible)
-pref = "ifd::conv_kernel<" + ", ".join(inst)
+dom = rf["kernel"]  # e.g. conv_stream2_kernel<0> or conv_kernel<256,64,4,1,9,0>
+kname, args = dom[:-1].split("<", 1)
+# rocprof names: "void ifd::conv_kernel<256, 64, 4, 1, 9, 0, 4, true>(ifd::ConvParams)" (extra args
+# possible), "void ifd::(anonymous namespace)::conv_stream2_kernel<0>(ifd::ConvParams)"
+pref = kname + "<" + ", ".join(args.split(","))
 rows = [r for r in csv.DictReader(open(os.path.join(out, "rocprof_kernel_stats.csv"))) if pref in r["Name"]]
 calls = sum(int(r["Calls"]) for r in rows)
 tot_ns = sum(float(r["TotalDurationNs"]) for r in rows)
