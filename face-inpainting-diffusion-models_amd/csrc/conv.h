@@ -73,8 +73,13 @@ struct ConvParams {
   // sampler epilogue (EPI_DDIM / EPI_DDPM): all NCHW [N,3,H,W] except mask [N,1,H,W]
   float* img; const float* gt; const float* mask; const float* noise; const float* known;
   StepCoeffs sc;
-  // IFD_TRACE builds only: per-block timestamps, 8 x u64 per block (see conv.hip)
+  // IFD_TRACE builds only: per-block timestamps (see conv.hip / conv_stream.hip)
   unsigned long long* trace;
+  // optional GroupNorm granule statistics of the output (norm.hip): gstat[n][e][cout/4] =
+  // (mean, M2); e = the tile's index within its image (x4 + consumer wave in conv_stream2).
+  // Written only for single-image tiles without split-K (the host checks).
+  float* gstat;
+  int gstat_E;
 };
 
 // Launch with the tile configuration chosen from (cout, taps, xform). Returns hipError_t.

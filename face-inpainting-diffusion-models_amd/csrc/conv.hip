@@ -415,6 +415,32 @@ __global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvPar
           if (ok[i]) v[i] = rv[i] + v[i];
       }
     }
+    if constexpr (QPP == 16) {
+      if (!split && p.gstat) {
+        // GroupNorm granule statistics of the tile (single-image tiles only, host-checked): thread
+        // = (quad q, ITEMS pixels); merge lanes q, q+16, q+32, q+48, then the 8 waves in order
+        GStat g = gstat_xlanes16(gstat_of<ITEMS>(v));
+        __syncthreads();  // all reads of the staged tile are done: reuse it
+        if (lane < 16) {
+          tile[(wave * 16 + lane) * 3 + 0] = g.n;
+          tile[(wave * 16 + lane) * 3 + 1] = g.mean;
+          tile[(wave * 16 + lane) * 3 + 2] = g.m2;
+        }
+        __syncthreads();
+        if (tid < 16) {
+          GStat a = {tile[tid * 3], tile[tid * 3 + 1], tile[tid * 3 + 2]};
+#pragma unroll
+          for (int w = 1; w < NT / 64; ++w) {
+            const int o = (w * 16 + tid) * 3;
+            a = gmerge(a, GStat{tile[o], tile[o + 1], tile[o + 2]});
+          }
+          const int e = ty * p.tiles_x + tx;
+          float* o = p.gstat + (((size_t)n0 * p.gstat_E + e) * (p.cout / 4) + ct * QPP + tid) * 2;
+          o[0] = a.mean;
+          o[1] = a.m2;
+        }
+      }
+    }
     const size_t img_out = (size_t)p.H * p.W * p.cout;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i)

@@ -29,6 +29,45 @@ __device__ __forceinline__ void gst4(float* p, f32x4 v) { *(__attribute__((addre
 // at ~2e-6 max-abs from the reference). The producer waves bound the pipeline, so the short form.
 __device__ __forceinline__ float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
+// Chan-merge statistics (count, mean, M2) for the fused GroupNorm granules.
+struct GStat {
+  float n, mean, m2;
+};
+__device__ __forceinline__ GStat gmerge(GStat a, GStat b) {
+  const float n = a.n + b.n;
+  const float d = b.mean - a.mean;
+  const float f = b.n / n;
+  return {n, a.mean + d * f, a.m2 + b.m2 + d * d * a.n * f};
+}
+// two-pass statistics of K quads held in registers
+template <int K>
+__device__ __forceinline__ GStat gstat_of(const f32x4 (&v)[K]) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < K; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mean = s * (1.0f / (4 * K));
+  float m2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const f32x4 d = v[i] - mean;
+    m2 += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+  }
+  return {4.0f * K, mean, m2};
+}
+// merge the statistics of lanes l, l ^ 16, l ^ 32 (butterfly, symmetric: all four lanes end equal)
+__device__ __forceinline__ GStat gstat_xlanes16(GStat a) {
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1) {
+    GStat b;
+    b.n = __shfl_xor(a.n, off);
+    b.mean = __shfl_xor(a.mean, off);
+    b.m2 = __shfl_xor(a.m2, off);
+    const bool lo = (threadIdx.x & off) == 0;
+    a = lo ? gmerge(a, b) : gmerge(b, a);
+  }
+  return a;
+}
+
 constexpr int NT = 512;    // threads per block
 constexpr int NP_T = 256;  // producer threads (waves 4-7)
 

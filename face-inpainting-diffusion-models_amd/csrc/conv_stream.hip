@@ -516,6 +516,7 @@ __global__ __launch_bounds__(NT, 4) void conv_stream2_kernel(ConvParams p) {
       const rsrc_t rr = mkrsrc(p.res ? p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout : p.out);
       const int co = t.ct * SBN + 4 * q;
       const f32x4 bias4 = gld4(p.bias + co);
+      GStat gs = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int piece = 0; piece < 2 * T::MR; ++piece) {
         const int mr = piece >> 1, half = piece & 1;
@@ -540,12 +541,28 @@ __global__ __launch_bounds__(NT, 4) void conv_stream2_kernel(ConvParams p) {
             const int pp = (r & 3) + 8 * ((r >> 2) & 1) + 4 * h;  // pixel within the piece
             strip[pp * SLDE + nr * 32 + l32] = acc[mr][nr][r];
           }
+        f32x4 vals[4];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           f32x4 val = *(const lds_f4*)(strip + (prow + 4 * v) * SLDE + 4 * q);
           val = val + bias4;
           if (p.res) val = rv[v] + val;
           bst4(ro, goff[v], val);
+          vals[v] = val;
+        }
+        if (p.gstat) {
+          const GStat g = gstat_of<4>(vals);
+          gs = piece == 0 ? g : gmerge(gs, g);
+        }
+      }
+      if (p.gstat) {
+        // GroupNorm granule statistics: this wave's 64 pixels x quad q, one entry per wave
+        gs = gstat_xlanes16(gs);
+        if (lane < 16) {
+          const int e = ((t.y0 / STH) * p.tiles_x + t.x0 / STW) * 4 + wave;
+          float* o = p.gstat + (((size_t)t.n0 * p.gstat_E + e) * (p.cout / 4) + t.ct * 16 + q) * 2;
+          o[0] = gs.mean;
+          o[1] = gs.m2;
         }
       }
     };

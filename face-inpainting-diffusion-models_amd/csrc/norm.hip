@@ -189,4 +189,183 @@ int launch_gn(const float* p0, int c0, const float* p1, int c1, int N, int HW, c
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Granule statistics. Every activation tensor can carry per-(image, entry, channel quad)
+// partial statistics P[n][e][c/4] = (mean, M2) over `cnt` values (an entry = a fixed set of
+// pixels, the same for all granules). The convs that PRODUCE a tensor write them from their
+// epilogue (conv.hip / conv_stream.hip, ConvParams::gstat), so the GroupNorm of the next layer
+// needs no pass over the tensor; tensors without them get gn_granules_kernel (one streaming pass).
+// gn_finalize2 merges the entries of each granule and the granules of each group — across the
+// two concat sources when the GroupNorm input is cat(h, skip) — in float64, in a fixed order.
+
+struct GnGranuleParams {
+  const float* x; int C;
+  int HW;         // pixels per image
+  int slice;      // pixels per entry (block)
+  int E;          // entries per image
+  float* part;    // [N][E][C/4][2]
+};
+
+// one block per (entry, n): thread layout as gn_partial_kernel (channel quad x pixel lane),
+// shifted sums per thread, Chan merges over pixel lanes in a fixed order
+__global__ __launch_bounds__(GN_NT) void gn_granules_kernel(GnGranuleParams p) {
+  __shared__ float red[GN_NT * 3 * 4];
+  const int QPT = p.C >> 2;
+  const int PL = GN_NT / QPT;
+  const int tid = threadIdx.x;
+  const int q = tid % QPT, pl = tid / QPT;
+  const int n = blockIdx.y, s = blockIdx.x;
+  const int px0 = s * p.slice, px1 = min(px0 + p.slice, p.HW);
+  const bool active = pl < PL;
+  f32x4 K = {0.f, 0.f, 0.f, 0.f}, s1 = K, s2 = K;
+  float cnt = 0.f;
+  if (active) {
+    const float* base = p.x + (size_t)n * p.HW * p.C + 4 * q;
+    int px = px0 + pl;
+    if (px < px1) K = *reinterpret_cast<const f32x4*>(base + (size_t)px * p.C);
+#pragma unroll 4
+    for (; px < px1; px += PL) {
+      const f32x4 d = *reinterpret_cast<const f32x4*>(base + (size_t)px * p.C) - K;
+      s1 += d;
+      s2 += d * d;
+      cnt += 1.f;
+    }
+    // the quad's 4 channels as 4 stats, merged into one granule stat
+    Stat g = {0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) {
+      Stat st;
+      st.n = cnt;
+      st.mean = cnt > 0.f ? K[j] + s1[j] / cnt : 0.f;
+      st.m2 = cnt > 0.f ? fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f) : 0.f;
+      g = j == 0 ? st : merge(g, st);
+    }
+    red[(pl * QPT + q) * 3 + 0] = g.n;
+    red[(pl * QPT + q) * 3 + 1] = g.mean;
+    red[(pl * QPT + q) * 3 + 2] = g.m2;
+  }
+  __syncthreads();
+  for (int qq = tid; qq < QPT; qq += GN_NT) {
+    Stat a = {red[qq * 3], red[qq * 3 + 1], red[qq * 3 + 2]};
+    for (int l = 1; l < PL; ++l) {
+      const int o = (l * QPT + qq) * 3;
+      a = merge(a, Stat{red[o], red[o + 1], red[o + 2]});
+    }
+    float* o = p.part + (((size_t)n * p.E + s) * QPT + qq) * 2;
+    o[0] = a.mean;
+    o[1] = a.m2;
+  }
+}
+
+struct GnSrc {
+  const float* part;  // [N][E][C/4][2]
+  int E, C;
+  float cnt;          // values per (entry, granule)
+};
+
+struct GnFinalize2Params {
+  GnSrc s0, s1;       // s1.C == 0: single source
+  const float* gamma; const float* beta;
+  const float* emb;   // optional [N][emb_stride] scale at emb_off, shift at emb_off + C
+  int emb_stride, emb_off;
+  float eps;
+  float* A; float* B;  // [N][C]
+};
+
+__device__ __forceinline__ void merge64(double& n, double& m, double& m2, double nb, double mb, double m2b) {
+  const double tot = n + nb;
+  if (nb <= 0) return;
+  const double d = mb - m;
+  m += d * (nb / tot);
+  m2 += m2b + d * d * (n * nb / tot);
+  n = tot;
+}
+
+// one block per (group g, image n): for each granule of the group the 256 threads merge strided
+// entries in float64, a fixed-shape LDS tree merges the threads, and the granules are merged in
+// channel order; then the group's channels get A/B
+__global__ __launch_bounds__(GN_NT) void gn_finalize2_kernel(GnFinalize2Params p) {
+  __shared__ double rn[GN_NT], rm[GN_NT], r2[GN_NT];
+  __shared__ float sres[2];
+  const int g = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  const int C = p.s0.C + p.s1.C;
+  const int Cg = C / GN_G;
+  double gn = 0.0, gm = 0.0, gm2 = 0.0;
+  for (int c = g * Cg; c < (g + 1) * Cg; c += 4) {
+    const bool first = c < p.s0.C;
+    const GnSrc& S = first ? p.s0 : p.s1;
+    const int gr = (first ? c : c - p.s0.C) >> 2;
+    const int QP = S.C >> 2;
+    double cn = 0.0, cm = 0.0, cm2 = 0.0;
+    for (int e = tid; e < S.E; e += GN_NT) {
+      const float* o = S.part + (((size_t)n * S.E + e) * QP + gr) * 2;
+      merge64(cn, cm, cm2, (double)S.cnt, (double)o[0], (double)o[1]);
+    }
+    rn[tid] = cn;
+    rm[tid] = cm;
+    r2[tid] = cm2;
+    __syncthreads();
+    for (int w = GN_NT / 2; w > 0; w >>= 1) {
+      if (tid < w) {
+        double an = rn[tid], am = rm[tid], a2 = r2[tid];
+        merge64(an, am, a2, rn[tid + w], rm[tid + w], r2[tid + w]);
+        rn[tid] = an;
+        rm[tid] = am;
+        r2[tid] = a2;
+      }
+      __syncthreads();
+    }
+    if (gn == 0.0) {
+      gn = rn[0]; gm = rm[0]; gm2 = r2[0];
+    } else {
+      merge64(gn, gm, gm2, rn[0], rm[0], r2[0]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    sres[0] = (float)gm;
+    sres[1] = (float)(1.0 / sqrt(gm2 / gn + (double)p.eps));
+  }
+  __syncthreads();
+  const float mean = sres[0], rstd = sres[1];
+  for (int c = g * Cg + tid; c < (g + 1) * Cg; c += GN_NT) {
+    const float a = rstd * p.gamma[c];
+    const float b = p.beta[c] - mean * a;
+    float A = a, B = b;
+    if (p.emb) {
+      const float sc = 1.0f + p.emb[(size_t)n * p.emb_stride + p.emb_off + c];
+      const float sh = p.emb[(size_t)n * p.emb_stride + p.emb_off + C + c];
+      A = a * sc;
+      B = b * sc + sh;
+    }
+    p.A[(size_t)n * C + c] = A;
+    p.B[(size_t)n * C + c] = B;
+  }
+}
+
+int launch_gn_granules(const float* x, int C, int N, int HW, float* part, int* E, float* cnt, hipStream_t stream) {
+  GnGranuleParams gp;
+  gp.x = x; gp.C = C; gp.HW = HW;
+  gp.E = gn_slices(HW, &gp.slice);
+  gp.part = part;
+  IFD_REQUIRE(HW % gp.slice == 0, "granule entries must be equal-sized");
+  hipLaunchKernelGGL(gn_granules_kernel, dim3(gp.E, N), dim3(GN_NT), 0, stream, gp);
+  *E = gp.E;
+  *cnt = 4.0f * gp.slice;
+  return (int)hipGetLastError();
+}
+
+int launch_gn_finalize2(const float* part0, int E0, float cnt0, int C0, const float* part1, int E1, float cnt1,
+                        int C1, int N, const float* gamma, const float* beta, const float* emb, int emb_stride,
+                        int emb_off, float* A, float* B, hipStream_t stream) {
+  GnFinalize2Params fp;
+  fp.s0 = GnSrc{part0, E0, C0, cnt0};
+  fp.s1 = GnSrc{part1, E1, C1, cnt1};
+  fp.gamma = gamma; fp.beta = beta;
+  fp.emb = emb; fp.emb_stride = emb_stride; fp.emb_off = emb_off;
+  fp.eps = 1e-5f;
+  fp.A = A; fp.B = B;
+  hipLaunchKernelGGL(gn_finalize2_kernel, dim3(GN_G, N), dim3(GN_NT), 0, stream, fp);
+  return (int)hipGetLastError();
+}
+
 }  // namespace ifd

@@ -76,6 +76,17 @@ class Model {
   int run_res(const ResP& r, const float* in0, int c0, const float* in1, int c1, int N, int Hin, float* out,
               hipStream_t s);
   int run_attn(const AttnP& a, const float* in, int N, int Hin, float* out, hipStream_t s);
+  // GroupNorm coefficients A/B of cat(in0, in1) from the sources' granule statistics (fused into
+  // the producing conv's epilogue when it could, else one gn_granules pass per source)
+  int run_gn(const float* in0, int c0, const float* in1, int c1, int N, int HW, const GNW& gn, const float* emb,
+             int emb_stride, int emb_off, float* A, float* B, hipStream_t s);
+  struct StatRec {
+    float* part = nullptr;
+    int E = 0;
+    float cnt = 0.f;
+    int C = 0;
+  };
+  int stats_for(const float* buf, int C, int N, int HW, StatRec* out, hipStream_t s);
   int run_conv(const ConvW& cw, const float* in0, int c0, const float* in1, int c1, int N, int Hin, int H, int xf,
                int act, const float* A, const float* Bc, const float* s0, int sc0, const float* s1, int sc1,
                const float* res, int res_xf, int resH, float* out, int epi, hipStream_t s,
@@ -123,6 +134,11 @@ class Model {
          o_emb_ = 0, o_E_ = 0, o_split_ = 0;
   size_t split_floats_ = 0;
   std::vector<size_t> o_hs_;
+  // GroupNorm granule statistics: one area per activation buffer (hs, bufs, t1); stat_ holds the
+  // buffers whose current contents have valid statistics (reset per forward)
+  std::map<const float*, float*> stat_area_;
+  std::map<const float*, StatRec> stat_;
+  bool gn_fused_ = true;
 };
 
 }  // namespace ifd

@@ -461,11 +461,23 @@ int Model::ensure_workspace(int B) {
   o_split_ = reserve(std::max<size_t>(split_floats_, 64));
   o_emb_ = reserve((size_t)B * emb_dim_);
   o_E_ = reserve((size_t)B * emb_total_);
+  // granule statistics areas: a tensor at resolution r with C channels has at most
+  // max(r^2/64, 1) entries of C/4 (mean, M2) pairs per image
+  auto stat_floats = [&](int r, int C) { return (size_t)B * std::max(r * r / 64, 1) * (C / 4) * 2; };
+  std::vector<std::pair<size_t, size_t>> stat_of;  // (buffer offset, stat offset)
+  for (size_t i = 0; i < o_hs_.size(); ++i) stat_of.push_back({o_hs_[i], reserve(stat_floats(in_res_[i], in_ch_[i]))});
+  size_t worst = 0;
+  for (int r = 1; r <= R; r *= 2) worst = std::max(worst, stat_floats(r, (int)std::min<size_t>(maxC, 512)));
+  worst = std::max(worst, stat_floats(R, 512));
+  for (int k = 0; k < 3; ++k) stat_of.push_back({o_bufs_[k], reserve(worst)});
+  stat_of.push_back({o_t1_, reserve(worst)});
   if (ws_) IFD_CHECK_HIP(hipFree(ws_));
   ws_ = nullptr;
   IFD_CHECK_HIP(hipMalloc(&ws_, n * sizeof(float)));
   ws_floats_ = n;
   ws_B_ = B;
+  stat_area_.clear();
+  for (auto& so : stat_of) stat_area_[ws_ + so.first] = ws_ + so.second;
   return 0;
 }
 
@@ -499,6 +511,21 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   p.img = img; p.gt = gt; p.mask = mask; p.noise = noise; p.known = known;
   IFD_REQUIRE(c0 % 8 == 0 && c1 % 8 == 0 && c0 + c1 == cw.cin_pad, "conv input channels");
   IFD_REQUIRE(!cw.has_skip || (sc0 + sc1 == cw.cs_pad && sc0 % 8 == 0 && sc1 % 8 == 0), "skip channels");
+  // IFD_CONV_STREAM selects the wide-layer kernel: 0 one tile per workgroup (conv.hip), 1 one
+  // persistent workgroup per CU, 2 two persistent workgroups per CU (conv_stream.hip)
+  const char* st_env = getenv("IFD_CONV_STREAM");
+  const int stream_mode = st_env ? atoi(st_env) : kDefaultStreamMode;
+  const bool use_stream = stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn);
+  // fused GroupNorm statistics of the output (single-image tiles, no split-K; not mode 1)
+  p.gstat = nullptr;
+  p.gstat_E = 0;
+  if (gn_fused_ && epi == EPI_NHWC && p.ksplit == 1 && p.IMGS == 1 && cw.bn == 64 && (!use_stream || stream_mode == 2)) {
+    auto it = stat_area_.find(out);
+    if (it != stat_area_.end()) {
+      p.gstat = it->second;
+      p.gstat_E = p.tiles_x * p.tiles_y * (use_stream ? 4 : 1);
+    }
+  }
 #if IFD_TRACE
   // development builds: dump per-block timestamps of the IFD_TRACE_NTH launch whose layer name
   // contains IFD_TRACE_MATCH into IFD_TRACE_FILE (+ ".json" with the geometry)
@@ -523,12 +550,11 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
 #endif
   hipEvent_t e0;
   prof_begin(s, &e0);
-  // IFD_CONV_STREAM selects the wide-layer kernel: 0 one tile per workgroup (conv.hip), 1 one
-  // persistent workgroup per CU, 2 two persistent workgroups per CU (conv_stream.hip)
-  const char* st_env = getenv("IFD_CONV_STREAM");
-  const int stream_mode = st_env ? atoi(st_env) : kDefaultStreamMode;
-  const bool use_stream = stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn);
   int e = use_stream ? launch_conv_stream(p, xf, stream_mode, s) : launch_conv(p, cw.taps, xf, cw.bn, s);
+  if (p.gstat)
+    stat_[out] = StatRec{p.gstat, p.gstat_E, 4.0f * (use_stream ? 64 : p.bm), cw.cout};
+  else
+    stat_.erase(out);
 #if IFD_TRACE
   if (tbuf) {
     IFD_CHECK_HIP(hipStreamSynchronize(s));
@@ -579,6 +605,36 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
 
 static double gn_bytes(int N, int HW, int C) { return 4.0 * 2.0 * N * (double)HW * C; }
 
+int Model::stats_for(const float* buf, int C, int N, int HW, StatRec* out, hipStream_t s) {
+  auto it = stat_.find(buf);
+  if (it != stat_.end() && it->second.C == C) {
+    *out = it->second;
+    return 0;
+  }
+  auto ar = stat_area_.find(buf);
+  IFD_REQUIRE(ar != stat_area_.end(), "GroupNorm input is not a workspace activation buffer");
+  StatRec r;
+  r.part = ar->second;
+  r.C = C;
+  int e = launch_gn_granules(buf, C, N, HW, r.part, &r.E, &r.cnt, s);
+  if (e) return e;
+  stat_[buf] = r;
+  *out = r;
+  return 0;
+}
+
+int Model::run_gn(const float* in0, int c0, const float* in1, int c1, int N, int HW, const GNW& gn, const float* emb,
+                  int emb_stride, int emb_off, float* A, float* B, hipStream_t s) {
+  if (!gn_fused_ || ((c0 + c1) / 32) % 4 != 0)  // granules are 4 channels: groups must hold whole ones
+    return launch_gn(in0, c0, in1, c1, N, HW, wblob_ + gn.g_off, wblob_ + gn.b_off, emb, emb_stride, emb_off,
+                     ws_ + o_part_, A, B, s);
+  StatRec r0, r1;
+  if (stats_for(in0, c0, N, HW, &r0, s)) return 1;
+  if (in1 && stats_for(in1, c1, N, HW, &r1, s)) return 1;
+  return launch_gn_finalize2(r0.part, r0.E, r0.cnt, c0, in1 ? r1.part : nullptr, r1.E, r1.cnt, in1 ? c1 : 0, N,
+                             wblob_ + gn.g_off, wblob_ + gn.b_off, emb, emb_stride, emb_off, A, B, s);
+}
+
 int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, int c1, int N, int Hin, float* out,
                    hipStream_t s) {
   float* A = ws_ + o_A_;
@@ -588,16 +644,15 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
   const int H = r.xf == XF_UP ? 2 * Hin : (r.xf == XF_DOWN ? Hin / 2 : Hin);
   hipEvent_t g0;
   prof_begin(s, &g0);
-  int e = launch_gn(in0, c0, in1, c1, N, Hin * Hin, wblob_ + r.gn1.g_off, wblob_ + r.gn1.b_off, nullptr, 0, 0, part, A,
-                    Bc, s);
+  (void)part;
+  int e = run_gn(in0, c0, in1, c1, N, Hin * Hin, r.gn1, nullptr, 0, 0, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, Hin * Hin, c0 + c1));
   IFD_REQUIRE(e == 0, "gn launch");
   if (run_conv(r.conv1, in0, c0, in1, c1, N, Hin, H, r.xf, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
                0, t1, EPI_NHWC, s))
     return 1;
   prof_begin(s, &g0);
-  e = launch_gn(t1, r.cout, nullptr, 0, N, H * H, wblob_ + r.gn2.g_off, wblob_ + r.gn2.b_off, ws_ + o_E_, emb_total_,
-                r.emb_off, part, A, Bc, s);
+  e = run_gn(t1, r.cout, nullptr, 0, N, H * H, r.gn2, ws_ + o_E_, emb_total_, r.emb_off, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, H * H, r.cout));
   IFD_REQUIRE(e == 0, "gn launch");
   const float* res = r.conv2.has_skip ? nullptr : in0;
@@ -613,8 +668,7 @@ int Model::run_attn(const AttnP& a, const float* in, int N, int Hin, float* out,
   const int T = Hin * Hin;
   hipEvent_t g0;
   prof_begin(s, &g0);
-  int e = launch_gn(in, a.C, nullptr, 0, N, T, wblob_ + a.gn.g_off, wblob_ + a.gn.b_off, nullptr, 0, 0,
-                    ws_ + o_part_, A, Bc, s);
+  int e = run_gn(in, a.C, nullptr, 0, N, T, a.gn, nullptr, 0, 0, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, T, a.C));
   IFD_REQUIRE(e == 0, "gn launch");
   if (run_conv(a.qkv, in, a.C, nullptr, 0, N, Hin, Hin, XF_NONE, ACT_AFFINE, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
@@ -641,6 +695,11 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   const int R = cfg_.image_size;
   const int mc = cfg_.model_channels;
   float* x0 = ws_ + o_x0_;
+  stat_.clear();
+  {
+    const char* gf = getenv("IFD_GN_FUSED");  // development switch: 0 = separate statistics pass
+    gn_fused_ = !(gf && gf[0] == '0');
+  }
   hipEvent_t p0;
   prof_begin(s, &p0);
   launch_pack_input(x, a, m, pack_mode, B, R * R, x0, s);
@@ -718,8 +777,7 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   float* A = ws_ + o_A_;
   float* Bc = ws_ + o_B_;
   prof_begin(s, &p0);
-  int e = launch_gn(cur, cur_c, nullptr, 0, B, R * R, wblob_ + gn_out_.g_off, wblob_ + gn_out_.b_off, nullptr, 0, 0,
-                    ws_ + o_part_, A, Bc, s);
+  int e = run_gn(cur, cur_c, nullptr, 0, B, R * R, gn_out_, nullptr, 0, 0, A, Bc, s);
   prof_end(s, p0, "groupnorm_stats", 0.0, gn_bytes(B, R * R, cur_c));
   IFD_REQUIRE(e == 0, "gn launch");
   return run_conv(conv_out_, cur, cur_c, nullptr, 0, B, R, R, XF_NONE, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0,

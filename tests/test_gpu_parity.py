@@ -98,13 +98,16 @@ def test_unet_batch_independent(evals, red_model):
 def test_stream_conv_bitwise(full_model, mode):
     """The persistent streaming convs (wide layers; mode 1: one workgroup per CU, mode 2: two)
     and the one-tile-per-workgroup conv sum in the same order: outputs must be bit-identical.
-    B=3 256x256 also exercises tile counts that are not multiples of the grid."""
+    B=3 256x256 also exercises tile counts that are not multiples of the grid. GroupNorm
+    statistics come from the separate pass here (IFD_GN_FUSED=0): the fused ones are merged per
+    epilogue entry, whose shape differs between the kernels (covered by the golden tests)."""
     g = torch.Generator(device=DEV).manual_seed(3)
     x = torch.randn(3, 3, 256, 256, device=DEV, generator=g)
     gt = torch.rand(3, 3, 256, 256, device=DEV, generator=g) * 2 - 1
     mask = (torch.rand(3, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
     t = torch.tensor([999, 500, 3], device=DEV)
     old = os.environ.get("IFD_CONV_STREAM")
+    os.environ["IFD_GN_FUSED"] = "0"
     try:
         with torch.no_grad():
             os.environ["IFD_CONV_STREAM"] = mode
@@ -112,6 +115,7 @@ def test_stream_conv_bitwise(full_model, mode):
             os.environ["IFD_CONV_STREAM"] = "0"
             y0 = full_model(x, t, masked_image=gt * (1 - mask), mask=mask).clone()
     finally:
+        os.environ.pop("IFD_GN_FUSED", None)
         if old is None:
             os.environ.pop("IFD_CONV_STREAM", None)
         else:
