@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--eta", type=float, default=0.75)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--precision", choices=["fp32", "3xf16"], default="fp32",
+                    help="conv arithmetic: exact fp32 MFMA, or the fp32-accurate 3xf16 split MFMA")
     args = ap.parse_args()
 
     from ifd import parallel
@@ -107,7 +109,7 @@ def main():
     parallel.init(device=dev)
     B, H = args.batch, FULL.image_size
 
-    model = DiffusionInpaintingModel(FULL, device=dev)
+    model = DiffusionInpaintingModel(FULL, device=dev, precision=args.precision)
     model.load_state_dict(make_state_dict(FULL, seed=1))
     model.eval()
     diffusion = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="cosine")
@@ -149,7 +151,7 @@ def main():
         _lib.check(L.ifd_profile_report(handle.h, cbuf, len(cbuf)))
         _lib.check(L.ifd_profile_enable(handle.h, 0))
         kernels = json.loads(cbuf.value.decode())["kernels"]
-        conv = {k: v for k, v in kernels.items() if k.startswith("conv_kernel")}
+        conv = {k: v for k, v in kernels.items() if k.startswith("conv_")}
         dom = max(conv, key=lambda k: conv[k]["ms"])
         d = conv[dom]
         achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12

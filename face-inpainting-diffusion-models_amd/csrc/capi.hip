@@ -22,7 +22,7 @@ using ifd::set_error;
 extern "C" {
 
 const char* ifd_last_error(void) { return ifd::get_error(); }
-const char* ifd_version(void) { return "ifd 0.1 gfx950 fp32-mfma"; }
+const char* ifd_version(void) { return "ifd 0.2 gfx950 fp32-mfma + 3xf16-split-mfma"; }
 
 int ifd_create(const ifd_config* cfg, ifd_handle** out) {
   if (!cfg || !out) {
@@ -75,6 +75,17 @@ int ifd_load_weights(ifd_handle* h, const char* name, const float* data, const i
 int ifd_finalize(ifd_handle* h) {
   if (!h) { set_error("null handle"); return 2; }
   return h->model->finalize();
+}
+
+int ifd_set_precision(ifd_handle* h, int prec) {
+  if (!h) { set_error("null handle"); return 2; }
+  return h->model->set_precision(prec);
+}
+
+int ifd_get_precision(ifd_handle* h, int* prec) {
+  if (!h || !prec) { set_error("null argument"); return 2; }
+  *prec = h->model->precision();
+  return 0;
 }
 
 int ifd_memory(ifd_handle* h, int64_t* wb, int64_t* ws) {

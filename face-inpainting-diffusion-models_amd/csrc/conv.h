@@ -91,6 +91,9 @@ int launch_splitk_reduce(const ConvParams& p, hipStream_t stream);
 // Persistent streaming kernel for the wide layers (conv_stream.hip).
 bool conv_stream_eligible(const ConvParams& p, int taps, int xform, int bn);
 int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t stream);
+// 3xf16 split-precision streaming kernel (conv_x3.hip); wpack = the x3 packing (pack_conv_x3).
+bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn);
+int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream);
 
 // Shared elementwise step math, also used by the standalone step kernels (sampler.hip).
 __device__ __forceinline__ float ddim_step_value(const StepCoeffs& s, float img, float eps, float noise,

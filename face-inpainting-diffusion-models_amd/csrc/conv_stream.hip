@@ -62,43 +62,6 @@ constexpr int EPI_PIECES = 4;                     // 64-pixel pieces, one per co
 #define BARRIER_CONSUMER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #define BARRIER_PRODUCER(N) asm volatile("s_waitcnt vmcnt(" #N ") lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-struct STile {
-  int n0, y0, x0, ct;
-};
-
-__device__ __forceinline__ STile decode_tile(const ConvParams& p, int L, int nct) {
-  const int grp = L / (8 * nct), rr = L - grp * 8 * nct;
-  STile t;
-  t.ct = rr >> 3;
-  int bx = grp * 8 + (rr & 7);
-  const int tx = bx % p.tiles_x;
-  bx /= p.tiles_x;
-  const int ty = bx % p.tiles_y;
-  t.n0 = bx / p.tiles_y;
-  t.y0 = ty * STH;
-  t.x0 = tx * STW;
-  return t;
-}
-
-// gfx950 executes v_mfma_f32_32x32x2_f32 on the vector ALUs: a producer's VALU instruction
-// issues only between MFMAs of the consumer beside it on the SIMD, so every producer VALU cycle
-// is a matrix cycle lost (per-interval stamps: interval = MFMA time + producer busy time). The
-// producer therefore does its address work once per TILE: loads go through buffer descriptors
-// (SGPR base per tile + per-lane 32-bit offset fixed for the tile + scalar chunk offset), so a
-// chunk's loads cost no VALU at all; what remains per chunk is the activation math itself.
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-__device__ __forceinline__ rsrc_t mkrsrc(const float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7ffffff0, 0x00020000);
-}
-__device__ __forceinline__ f32x4 bld4(rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
-__device__ __forceinline__ void bst4(rsrc_t r, int voff, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, voff,
-                                         0, 0);
-}
-
 template <int XF>
 struct SSet {
   f32x4 raw[SITEMS];

@@ -15,6 +15,8 @@ struct ConvW {
   int cs = 0, cs_pad = 0;          // 1x1 skip segment input channels
   size_t ws_off = 0;
   bool has_skip = false;
+  size_t x3_off = 0;   // float offset of the 3xf16 split packing (pack_conv_x3), 0 if none
+  bool x3_ok = false;  // every weight within the split's range (|w| < 32): the layer may run 3xf16
   std::string wname, bname, swname, sbname;  // source parameter names
 };
 
@@ -68,6 +70,9 @@ class Model {
   int profile_enable(int on);
   int profile_report(std::string& json);
   int64_t workspace_bytes() const { return (int64_t)ws_floats_ * 4; }
+  // Conv arithmetic: IFD_PREC_FP32 (exact fp32 MFMA) or IFD_PREC_3XF16 (split f16 MFMA, fp32-accurate)
+  int set_precision(int prec);
+  int precision() const { return prec_; }
 
  private:
   void build_plan();
@@ -139,6 +144,7 @@ class Model {
   std::map<const float*, float*> stat_area_;
   std::map<const float*, StatRec> stat_;
   bool gn_fused_ = true;
+  int prec_ = 0;
 };
 
 }  // namespace ifd

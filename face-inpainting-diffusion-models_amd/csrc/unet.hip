@@ -279,6 +279,45 @@ static void pack_conv(const std::vector<float>& w, int cout, int cin, int taps, 
             }
 }
 
+// 3xf16 split packing: [Cout_pad/BN][Cin_pad/16][taps][part][h][BN][8] f16 (2 per float slot),
+// element (part, h, col, j) of (ct, chunk, tap) = split part of W[ct*BN + col][chunk*16 + 8h + j][tap]:
+// part 0 = f16(w) * 2^11 (exact), part 1 = f16((w - f16(w)) * 2^11) (conv_x3.hip). Returns false
+// if a weight is outside the scaled part's f16 range (|w| >= 32), leaving the layer on fp32.
+static bool pack_conv_x3(const std::vector<float>& w, int cout, int cin, int taps, int bn, int cin_pad16,
+                         int cout_pad, std::vector<float>& blob, size_t off) {
+  const int nch = cin_pad16 / 16;
+  _Float16* dst = reinterpret_cast<_Float16*>(blob.data() + off);
+  bool ok = true;
+  for (int ct = 0; ct < cout_pad / bn; ++ct)
+    for (int chk = 0; chk < nch; ++chk)
+      for (int tap = 0; tap < taps; ++tap)
+        for (int part = 0; part < 2; ++part)
+          for (int hh = 0; hh < 2; ++hh)
+            for (int col = 0; col < bn; ++col)
+              for (int j = 0; j < 8; ++j) {
+                const int co = ct * bn + col, ci = chk * 16 + hh * 8 + j;
+                float v = 0.f;
+                if (co < cout && ci < cin) v = w[((size_t)co * cin + ci) * taps + tap];
+                const _Float16 hi = (_Float16)v;
+                _Float16 o;
+                if (part == 0) {
+                  const float s = (float)hi * 2048.0f;
+                  if (!(std::fabs(s) <= 65504.0f)) ok = false;
+                  o = (_Float16)s;
+                } else {
+                  o = (_Float16)((v - (float)hi) * 2048.0f);
+                }
+                dst[((((((size_t)ct * nch + chk) * taps + tap) * 2 + part) * 2 + hh) * bn + col) * 8 + j] = o;
+              }
+  return ok;
+}
+
+int Model::set_precision(int prec) {
+  IFD_REQUIRE(prec == IFD_PREC_FP32 || prec == IFD_PREC_3XF16, "unknown precision mode");
+  prec_ = prec;
+  return 0;
+}
+
 int Model::finalize() {
   for (auto& p : params_) IFD_REQUIRE(host_.count(p.name), "missing parameter " + p.name);
   // size the blob
@@ -292,6 +331,10 @@ int Model::finalize() {
     c.w_off = reserve((size_t)c.cout_pad * c.cin_pad * c.taps);
     c.b_off = reserve(c.cout_pad);
     if (c.has_skip) c.ws_off = reserve((size_t)c.cout_pad * c.cs_pad);
+    // 3xf16 packing (two f16 parts = one float slot per weight) for the layers conv_x3 can run
+    c.x3_off = 0;
+    if (c.taps == 9 && c.bn == 64 && c.cin_pad % 16 == 0)
+      c.x3_off = reserve((size_t)c.cout_pad * c.cin_pad * c.taps);
   };
   auto plan_gn = [&](GNW& g) {
     g.g_off = reserve(g.C);
@@ -324,6 +367,8 @@ int Model::finalize() {
   auto put = [&](size_t off, const std::vector<float>& v) { std::copy(v.begin(), v.end(), blob.begin() + off); };
   auto fill_conv = [&](ConvW& c) {
     pack_conv(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob, c.w_off);
+    c.x3_ok = c.x3_off && pack_conv_x3(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob,
+                                       c.x3_off);
     const auto& b = host_[c.bname];
     for (int i = 0; i < c.cout; ++i) blob[c.b_off + i] = b[i];
     if (c.has_skip) {
@@ -515,11 +560,14 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   // persistent workgroup per CU, 2 two persistent workgroups per CU (conv_stream.hip)
   const char* st_env = getenv("IFD_CONV_STREAM");
   const int stream_mode = st_env ? atoi(st_env) : kDefaultStreamMode;
-  const bool use_stream = stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn);
+  const bool use_x3 = prec_ == IFD_PREC_3XF16 && cw.x3_ok && conv_x3_eligible(p, cw.taps, xf, cw.bn);
+  if (use_x3) p.wpack = wblob_ + cw.x3_off;
+  const bool use_stream = use_x3 || (stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn));
   // fused GroupNorm statistics of the output (single-image tiles, no split-K; not mode 1)
   p.gstat = nullptr;
   p.gstat_E = 0;
-  if (gn_fused_ && epi == EPI_NHWC && p.ksplit == 1 && p.IMGS == 1 && cw.bn == 64 && (!use_stream || stream_mode == 2)) {
+  if (gn_fused_ && epi == EPI_NHWC && p.ksplit == 1 && p.IMGS == 1 && cw.bn == 64 &&
+      (!use_stream || use_x3 || stream_mode == 2)) {
     auto it = stat_area_.find(out);
     if (it != stat_area_.end()) {
       p.gstat = it->second;
@@ -550,7 +598,9 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
 #endif
   hipEvent_t e0;
   prof_begin(s, &e0);
-  int e = use_stream ? launch_conv_stream(p, xf, stream_mode, s) : launch_conv(p, cw.taps, xf, cw.bn, s);
+  int e = use_x3       ? launch_conv_x3(p, xf, s)
+          : use_stream ? launch_conv_stream(p, xf, stream_mode, s)
+                       : launch_conv(p, cw.taps, xf, cw.bn, s);
   if (p.gstat)
     stat_[out] = StatRec{p.gstat, p.gstat_E, 4.0f * (use_stream ? 64 : p.bm), cw.cout};
   else
@@ -585,8 +635,11 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                                 (cw.has_skip ? pix * cw.cs : 0) + (res ? pix * cw.cout : 0));
     char nm[160];
     if (prof_layers_)
-      snprintf(nm, sizeof(nm), "%s<%d,%d,%d,%d> r%d %d+%d->%d skip%d", use_stream ? "conv_stream" : "conv_kernel", p.bm,
+      snprintf(nm, sizeof(nm), "%s<%d,%d,%d,%d> r%d %d+%d->%d skip%d",
+               use_x3 ? "conv_x3" : (use_stream ? "conv_stream" : "conv_kernel"), p.bm,
                cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
+    else if (use_x3)
+      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d>", xf);
     else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
       snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
     else if (use_stream)

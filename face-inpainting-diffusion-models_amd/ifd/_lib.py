@@ -53,6 +53,8 @@ EXPORTS = {
     "ifd_load_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, c_i64p, ctypes.c_int]),
     "ifd_finalize": (ctypes.c_int, [ctypes.c_void_p]),
     "ifd_memory": (ctypes.c_int, [ctypes.c_void_p, c_i64p, c_i64p]),
+    "ifd_set_precision": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ifd_get_precision": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "ifd_unet_forward": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int,
                                                                                       ctypes.c_int, ctypes.c_void_p,
                                                                                       ctypes.c_void_p]),
@@ -67,6 +69,9 @@ EXPORTS = {
     "ifd_blend": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                          ctypes.c_void_p, ctypes.c_void_p]),
 }
+
+# conv arithmetic modes (include/ifd.h IFD_PREC_*)
+PRECISIONS = {"fp32": 0, "3xf16": 1}
 
 _lib = None
 

@@ -75,9 +75,13 @@ class Handle:
 class DiffusionInpaintingModel(torch.nn.Module):
     """9-channel inpainting UNet (code/unet.py:176-200) executed by libifd."""
 
-    def __init__(self, cfg: UNetConfig = FULL, device=None):
+    def __init__(self, cfg: UNetConfig = FULL, device=None, precision: str = "fp32"):
         super().__init__()
         self.cfg = cfg
+        if precision not in _lib.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}")
+        # "fp32": exact fp32 MFMA; "3xf16": split f16 MFMA with fp32-level error (include/ifd.h)
+        self.precision = precision
         self.base_model = _Node()
         for key, shape in state_dict_spec(cfg, prefix=""):
             node = self.base_model
@@ -121,6 +125,7 @@ class DiffusionInpaintingModel(torch.nn.Module):
                     del t
                 _lib.check(L.ifd_finalize(self._handle.h))
             self._dirty = False
+        _lib.check(_lib.lib().ifd_set_precision(self._handle.h, _lib.PRECISIONS[self.precision]))
         return self._handle
 
     # -- forward -------------------------------------------------------------------------------

@@ -69,6 +69,16 @@ int ifd_param_info(ifd_handle* h, int i, const char** name, int64_t* shape4, int
 int ifd_load_weights(ifd_handle* h, const char* name, const float* data, const int64_t* shape, int ndim);
 /* Pack every loaded parameter into the device layouts. Missing parameters are an error. */
 int ifd_finalize(ifd_handle* h);
+/* Conv arithmetic of the handle (default IFD_PREC_FP32):
+ *   IFD_PREC_FP32   every conv on v_mfma_f32_32x32x2_f32: an exact fp32 fma chain.
+ *   IFD_PREC_3XF16  layers with a split kernel run each fp32 operand as two f16 parts (hi + 2^-11 lo)
+ *                   and three f16 MFMAs into one fp32 accumulator: fp32-level error,
+ *                   5.3x the fp32 MFMA rate; the other layers stay fp32. Takes effect on the next call.
+ * The reference has no such switch: its model runs in the caller's dtype (fp32 on this path). */
+#define IFD_PREC_FP32 0
+#define IFD_PREC_3XF16 1
+int ifd_set_precision(ifd_handle* h, int prec);
+int ifd_get_precision(ifd_handle* h, int* prec);
 /* Bytes of device workspace the handle holds (weights + activations). */
 int ifd_memory(ifd_handle* h, int64_t* weight_bytes, int64_t* workspace_bytes);
 

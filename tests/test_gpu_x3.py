@@ -1,0 +1,114 @@
+"""GPU parity of the 3xf16 split-precision mode (precision="3xf16", include/ifd.h IFD_PREC_3XF16).
+
+The same golden fixtures and tolerances as the fp32 mode (test_gpu_parity.py): the split path is
+claimed fp32-accurate, so it gets no looser bound. Every test also checks that the split kernel
+actually ran (profiler report names conv_x3_kernel), so a silent fallback to fp32 cannot pass.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from ifd.manifest import make_state_dict
+from ifd.topology import FULL
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def maxabs(a, b):
+    return float((a.double().cpu() - b.double().cpu()).abs().max())
+
+
+@pytest.fixture(scope="module")
+def x3_model():
+    from ifd.model import DiffusionInpaintingModel
+    m = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16")
+    m.load_state_dict(make_state_dict(FULL, seed=1))
+    return m.eval()
+
+
+def _kernels_run(model, fn):
+    from ifd import _lib
+    h = model.handle(DEV)
+    L = _lib.lib()
+    _lib.check(L.ifd_profile_enable(h.h, 1))
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        buf = ctypes.create_string_buffer(1 << 16)
+        _lib.check(L.ifd_profile_report(h.h, buf, len(buf)))
+    finally:
+        _lib.check(L.ifd_profile_enable(h.h, 0))
+    return out, json.loads(buf.value.decode())["kernels"]
+
+
+def test_x3_precision_switch(x3_model):
+    from ifd import _lib
+    h = x3_model.handle(DEV)
+    v = ctypes.c_int()
+    _lib.check(_lib.lib().ifd_get_precision(h.h, ctypes.byref(v)))
+    assert v.value == _lib.PRECISIONS["3xf16"]
+    with pytest.raises(RuntimeError):
+        _lib.check(_lib.lib().ifd_set_precision(h.h, 7))
+
+
+def test_x3_unet_full(evals, x3_model):
+    x, gt, mask = (_t(evals[f"full/{k}"]).to(DEV) for k in ("x", "gt", "mask"))
+    t = torch.tensor([999], device=DEV)
+    with torch.no_grad():
+        y, ks = _kernels_run(x3_model, lambda: x3_model(x, t, masked_image=gt * (1 - mask), mask=mask))
+    assert any(k.startswith("conv_x3_kernel") for k in ks), sorted(ks)
+    err = maxabs(y, _t(evals["full_t999/y"]))
+    print(f"3xf16 unet full t=999 maxabs={err:.3g}")
+    assert err <= 2e-5
+
+
+def test_x3_matches_fp32_batch(x3_model):
+    """B=3 random inputs (tile counts not a multiple of the grid) at three timesteps: the split
+    mode against the fp32 mode of the same weights."""
+    from ifd.model import DiffusionInpaintingModel
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(3, 3, 256, 256, device=DEV, generator=g)
+    gt = torch.rand(3, 3, 256, 256, device=DEV, generator=g) * 2 - 1
+    mask = (torch.rand(3, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
+    t = torch.tensor([999, 500, 3], device=DEV)
+    m32 = DiffusionInpaintingModel(FULL, device=DEV)
+    m32.load_state_dict(make_state_dict(FULL, seed=1))
+    with torch.no_grad():
+        y3 = x3_model(x, t, masked_image=gt * (1 - mask), mask=mask)
+        y32 = m32(x, t, masked_image=gt * (1 - mask), mask=mask)
+    assert torch.isfinite(y3).all()
+    err = maxabs(y3, y32)
+    print(f"3xf16 vs fp32 B=3 maxabs={err:.3g}")
+    assert err <= 2e-5
+    # images stay independent under the split path as well
+    with torch.no_grad():
+        y1 = x3_model(x[1:2], t[1:2], masked_image=(gt * (1 - mask))[1:2], mask=mask[1:2])
+    assert maxabs(y1, y3[1:2]) <= 2e-5
+
+
+@pytest.mark.parametrize("name", ["c1_full_cos10_eta0.9", "c1_full_cos10_eta0"])
+def test_x3_script_ddim_full_c1(loops, meta, x3_model, name):
+    """C1 loops under the split mode, held to the same oracle-envelope bound as the fp32 mode
+    (test_gpu_parity.py::test_script_ddim_full_c1)."""
+    from test_gpu_parity import _run_script_loop
+    cond = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "conditioning.json")))
+    env = [v for k, v in cond.items() if k.startswith(name + "/rel1e-05")]
+    env_max = max(v["max"] for v in env)
+    env_frac = max(v["frac_gt_1e-4"] for v in env)
+    env_p999 = max(v["p999"] for v in env)
+    lm = meta["loops"][name]
+    gt, mask = _t(loops[f"{name}/gt"]), _t(loops[f"{name}/mask"])
+    y = _run_script_loop(x3_model, lm, gt, mask)
+    d = (y.double().cpu() - _t(loops[f"{name}/y"]).double()).abs().flatten()
+    err, p999, frac = float(d.max()), float(d.quantile(0.999)), float((d > 1e-4).double().mean())
+    print(f"3xf16 {name}: maxabs={err:.3g} p99.9={p999:.3g} frac>1e-4={frac:.2e}")
+    assert err <= max(1e-3, env_max) and p999 <= max(1e-4, env_p999) and frac <= max(env_frac, 1e-5)

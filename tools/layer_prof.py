@@ -8,7 +8,7 @@ from ifd.model import DiffusionInpaintingModel
 from ifd.topology import FULL
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 dev = torch.device("cuda:0")
-m = DiffusionInpaintingModel(FULL, device=dev); m.load_state_dict(make_state_dict(FULL, seed=1))
+m = DiffusionInpaintingModel(FULL, device=dev, precision=sys.argv[2] if len(sys.argv) > 2 else "fp32"); m.load_state_dict(make_state_dict(FULL, seed=1))
 x = torch.randn(B, 3, 256, 256, device=dev); mk = (torch.rand(B, 1, 256, 256, device=dev) > 0.5).float()
 t = torch.full((B,), 500, device=dev)
 with torch.no_grad():
