@@ -86,7 +86,7 @@ struct ConvParams {
 int launch_conv(const ConvParams& p, int taps, int xform, int bn, hipStream_t stream);
 int conv_pick_bn(int cout, int taps, int H, int W, int N);
 // Tile geometry + split-K choice shared by the launcher and the workspace planner.
-void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks);
+void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool x3 = false);
 int launch_splitk_reduce(const ConvParams& p, hipStream_t stream);
 // Persistent streaming kernel for the wide layers (conv_stream.hip).
 bool conv_stream_eligible(const ConvParams& p, int taps, int xform, int bn);

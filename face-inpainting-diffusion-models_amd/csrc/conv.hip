@@ -560,13 +560,13 @@ int conv_pick_bn(int cout, int taps, int H, int W, int N) {
 // Tile geometry + split-K. BM = 256 (8 rows x 32 columns of one image) where the layer is wide and
 // the grid still gives >= 2 blocks per CU: it halves the weight-slab loads per MFMA, the producer's
 // bottleneck. Otherwise BM = 128, with split-K to cover the chip on the low-resolution layers.
-void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks) {
+void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool x3) {
   static const char* ov = getenv("IFD_CONV_BM");  // development override: 128 disables BM=256
   const bool allow256 = !(ov && atoi(ov) == 128);
   int bm = 128;
   if (allow256 && bn == 64 && W >= 32 && H >= 8) {
     const long blocks256 = (long)N * (H / 8) * (W / 32) * (p.cout_pad / bn);
-    if (blocks256 >= 512) bm = 256;
+    if (blocks256 >= 512 || x3) bm = 256;  // x3: persistent kernel, any tile count
   }
   p.bm = bm;
   p.TW = W < 32 ? W : 32;
@@ -581,7 +581,7 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks) {
   const long blocks = (long)p.npix_tiles * (p.cout_pad / bn);
   // split K until the grid covers ~2 blocks per CU, keeping >= 4 chunks per split
   int S = 1;
-  while (S < 8 && blocks * S < 512 && nchunks / (2 * S) >= 4) S *= 2;
+  while (!(x3 && bm == 256) && S < 8 && blocks * S < 512 && nchunks / (2 * S) >= 4) S *= 2;
   p.ksplit = S;
 }
 

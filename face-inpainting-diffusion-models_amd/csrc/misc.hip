@@ -1,6 +1,7 @@
 // Small kernels around the conv core: input assembly, timestep embedding + MLP, the batched
 // ResBlock emb projections, QKV attention, and the standalone sampler step / blend kernels.
 #include "conv.h"
+#include "conv_dev.h"
 #include "kernels.h"
 
 namespace ifd {
@@ -251,6 +252,50 @@ void launch_blend(const float* res, const float* gt, const float* mask, float* o
                   hipStream_t s) {
   const int tot = N * C * HW;
   hipLaunchKernelGGL(blend_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, res, gt, mask, out, N, C, HW);
+}
+
+// act + 2x2 average pool, 4 channels per thread (16-byte loads/stores, coalesced along C).
+__global__ __launch_bounds__(256) void act_pool_kernel(const float* __restrict__ x, int C, int N, int Hin, int act,
+                                                       const float* __restrict__ A, const float* __restrict__ B,
+                                                       float* __restrict__ out) {
+  const int Ho = Hin / 2, Q = C / 4;
+  const size_t tot = (size_t)N * Ho * Ho * Q;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int q = (int)(i % Q);
+  const size_t pix = i / Q;
+  const int xo = (int)(pix % Ho), yo = (int)((pix / Ho) % Ho), n = (int)(pix / ((size_t)Ho * Ho));
+  const float* b = x + (((size_t)n * Hin + 2 * yo) * Hin + 2 * xo) * C + 4 * q;
+  const f32x4 v00 = *(const f32x4*)b, v01 = *(const f32x4*)(b + C);
+  const f32x4 v10 = *(const f32x4*)(b + (size_t)Hin * C), v11 = *(const f32x4*)(b + (size_t)Hin * C + C);
+  f32x4 a = {1.f, 1.f, 1.f, 1.f}, c = {0.f, 0.f, 0.f, 0.f};
+  if (act != ACT_NONE) {
+    a = *(const f32x4*)(A + (size_t)n * C + 4 * q);
+    c = *(const f32x4*)(B + (size_t)n * C + 4 * q);
+  }
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    auto f = [&](float v) {
+      if (act == ACT_NONE) return v;
+      const float t = a[j] * v + c[j];
+      return act == ACT_AFFINE_SILU ? silu_fast(t) : t;
+    };
+    float s = f(v00[j]);
+    s = s + f(v01[j]);
+    s = s + f(v10[j]);
+    s = s + f(v11[j]);
+    r[j] = s * 0.25f;
+  }
+  *(f32x4*)(out + pix * C + 4 * q) = r;
+}
+
+int launch_act_pool(const float* x, int C, int N, int Hin, int act, const float* A, const float* B, float* out,
+                    hipStream_t s) {
+  const size_t tot = (size_t)N * (Hin / 2) * (Hin / 2) * (C / 4);
+  hipLaunchKernelGGL(act_pool_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, x, C, N, Hin, act, A, B,
+                     out);
+  return (int)hipGetLastError();
 }
 
 }  // namespace ifd

@@ -332,9 +332,11 @@ int Model::finalize() {
     c.b_off = reserve(c.cout_pad);
     if (c.has_skip) c.ws_off = reserve((size_t)c.cout_pad * c.cs_pad);
     // 3xf16 packing (two f16 parts = one float slot per weight) for the layers conv_x3 can run
-    c.x3_off = 0;
-    if (c.taps == 9 && c.bn == 64 && c.cin_pad % 16 == 0)
+    c.x3_off = c.x3s_off = 0;
+    if (c.taps == 9 && c.bn == 64 && c.cin_pad % 16 == 0 && (!c.has_skip || c.cs_pad % 16 == 0)) {
       c.x3_off = reserve((size_t)c.cout_pad * c.cin_pad * c.taps);
+      if (c.has_skip) c.x3s_off = reserve((size_t)c.cout_pad * c.cs_pad);
+    }
   };
   auto plan_gn = [&](GNW& g) {
     g.g_off = reserve(g.C);
@@ -369,6 +371,8 @@ int Model::finalize() {
     pack_conv(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob, c.w_off);
     c.x3_ok = c.x3_off && pack_conv_x3(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob,
                                        c.x3_off);
+    if (c.x3_ok && c.has_skip)
+      c.x3_ok = pack_conv_x3(host_[c.swname], c.cout, c.cs, 1, c.bn, c.cs_pad, c.cout_pad, blob, c.x3s_off);
     const auto& b = host_[c.bname];
     for (int i = 0; i < c.cout; ++i) blob[c.b_off + i] = b[i];
     if (c.has_skip) {
@@ -504,6 +508,14 @@ int Model::ensure_workspace(int B) {
       consider(a.proj, H);
     }
   o_split_ = reserve(std::max<size_t>(split_floats_, 64));
+  // act+pool staging of the down-ResBlocks (3xf16 mode): B x (res/2)^2 x cin, worst over the plan
+  size_t maxpool = 64;
+  for (auto& blk : in_blocks_)
+    for (auto& L : blk)
+      if (L.kind == L_RES && res_[L.idx].xf == XF_DOWN)
+        maxpool = std::max(maxpool, (size_t)B * (L.res_in / 2) * (L.res_in / 2) * res_[L.idx].cin);
+  o_pool_ = reserve(maxpool);
+  o_pool2_ = reserve(maxpool);  // pooled residual (a down-ResBlock keeps cin == cout)
   o_emb_ = reserve((size_t)B * emb_dim_);
   o_E_ = reserve((size_t)B * emb_total_);
   // granule statistics areas: a tensor at resolution r with C channels has at most
@@ -548,7 +560,9 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   p.out = out;
   p.epi = epi;
   IFD_REQUIRE((H & (H - 1)) == 0, "spatial size must be a power of two");
-  conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8);
+  // the persistent split kernel takes 256-pixel tiles whatever the grid (no split-K)
+  const bool x3_geo = prec_ == IFD_PREC_3XF16 && cw.x3_ok && epi == EPI_NHWC;
+  conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8, x3_geo);
   if (epi != EPI_NHWC) p.ksplit = 1;
   p.part = ws_ + o_split_;
   IFD_REQUIRE(p.ksplit == 1 || (size_t)p.ksplit * N * H * H * cw.cout <= split_floats_, "split-K workspace");
@@ -560,8 +574,45 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   // persistent workgroup per CU, 2 two persistent workgroups per CU (conv_stream.hip)
   const char* st_env = getenv("IFD_CONV_STREAM");
   const int stream_mode = st_env ? atoi(st_env) : kDefaultStreamMode;
+  // 3xf16: the split kernel has no avg-pool prologue or residual; a down-ResBlock's convs read
+  // act+pool(x) / pool(x) materialised by act_pool at the output resolution instead (the same
+  // fp32 arithmetic as conv.hip's XF_DOWN paths)
+  if (prec_ == IFD_PREC_3XF16 && cw.x3_ok) {
+    const bool pool_in = xf == XF_DOWN && !in1;
+    const bool pool_res = res && res_xf == XF_DOWN;
+    ConvParams q = p;
+    if (pool_in) {
+      q.in0 = ws_ + o_pool_;
+      q.Hin = q.Win = H;
+      q.act = ACT_NONE;
+    }
+    if (pool_res) {
+      q.res = ws_ + o_pool2_;
+      q.res_xform = XF_NONE;
+      q.res_H = q.res_W = H;
+    }
+    if ((pool_in || pool_res) && conv_x3_eligible(q, cw.taps, pool_in ? (int)XF_NONE : xf, cw.bn)) {
+      hipEvent_t pe;
+      prof_begin(s, &pe);
+      int e = 0;
+      if (pool_in) e = launch_act_pool(in0, c0, N, Hin, act, A, Bc, ws_ + o_pool_, s);
+      if (!e && pool_res) e = launch_act_pool(res, cw.cout, N, resH, ACT_NONE, nullptr, nullptr, ws_ + o_pool2_, s);
+      prof_end(s, pe, "act_pool", 0.0, 4.0 * N * (double)Hin * Hin * (c0 + (pool_res ? cw.cout : 0)) * 1.25);
+      IFD_REQUIRE(e == 0, "act_pool launch");
+      p = q;
+      if (pool_in) {
+        xf = XF_NONE;
+        act = ACT_NONE;
+      }
+    }
+  }
   const bool use_x3 = prec_ == IFD_PREC_3XF16 && cw.x3_ok && conv_x3_eligible(p, cw.taps, xf, cw.bn);
-  if (use_x3) p.wpack = wblob_ + cw.x3_off;
+  if (use_x3) {
+    p.wpack = wblob_ + cw.x3_off;
+    if (cw.has_skip) p.wskip = wblob_ + cw.x3s_off;
+  } else if (x3_geo) {  // not split-eligible after all: the fp32 kernels' own geometry
+    conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8);
+  }
   const bool use_stream = use_x3 || (stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn));
   // fused GroupNorm statistics of the output (single-image tiles, no split-K; not mode 1)
   p.gstat = nullptr;
@@ -639,7 +690,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                use_x3 ? "conv_x3" : (use_stream ? "conv_stream" : "conv_kernel"), p.bm,
                cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
     else if (use_x3)
-      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d>", xf);
+      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s>", xf, cw.has_skip ? "true" : "false");
     else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
       snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
     else if (use_stream)
