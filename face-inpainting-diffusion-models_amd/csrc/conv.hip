@@ -564,9 +564,13 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
   static const char* ov = getenv("IFD_CONV_BM");  // development override: 128 disables BM=256
   const bool allow256 = !(ov && atoi(ov) == 128);
   int bm = 128;
-  if (allow256 && bn == 64 && W >= 32 && H >= 8) {
+  if (x3) {
+    // 3xf16 split kernel (conv_x3.hip): 256-pixel tiles of one image (8 x 32 or 16 x 16) whatever
+    // the tile count (persistent grid); nchunks = 16-channel chunks of the whole K stream
+    if (bn == 64 && W >= 16 && H >= 256 / (W < 32 ? W : 32)) bm = 256;
+  } else if (allow256 && bn == 64 && W >= 32 && H >= 8) {
     const long blocks256 = (long)N * (H / 8) * (W / 32) * (p.cout_pad / bn);
-    if (blocks256 >= 512 || x3) bm = 256;  // x3: persistent kernel, any tile count
+    if (blocks256 >= 512) bm = 256;
   }
   p.bm = bm;
   p.TW = W < 32 ? W : 32;
@@ -579,9 +583,14 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
   const int tiles_n = (N + p.IMGS - 1) / p.IMGS;
   p.npix_tiles = tiles_n * p.tiles_y * p.tiles_x;
   const long blocks = (long)p.npix_tiles * (p.cout_pad / bn);
-  // split K until the grid covers ~2 blocks per CU, keeping >= 4 chunks per split
   int S = 1;
-  while (!(x3 && bm == 256) && S < 8 && blocks * S < 512 && nchunks / (2 * S) >= 4) S *= 2;
+  if (x3 && bm == 256) {
+    // persistent units: split K until the units cover the 256 CUs, keeping >= 4 chunks per unit
+    while (S < 8 && blocks * S < 256 && nchunks % (2 * S) == 0 && nchunks / (2 * S) >= 4) S *= 2;
+  } else {
+    // split K until the grid covers ~2 blocks per CU, keeping >= 4 chunks per split
+    while (S < 8 && blocks * S < 512 && nchunks / (2 * S) >= 4) S *= 2;
+  }
   p.ksplit = S;
 }
 

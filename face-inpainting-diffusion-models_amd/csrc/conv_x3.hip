@@ -1,4 +1,4 @@
-// 3xf16 split-precision fused 3x3 convolution ("3xf16" precision mode) for the wide layers.
+// 3xf16 split-precision fused 3x3 convolution ("3xf16" precision mode).
 //
 // Why: gfx950 has no xf32, and v_mfma_f32_32x32x2_f32 runs at the fp32 VECTOR rate (157 TF/s),
 // sharing the VALU with the producer waves. The f16 matrix path is 16x faster per K. Each fp32
@@ -10,23 +10,30 @@
 //     acc += a_hi * (w_hi 2^11)  +  a_hi * w_lo'  +  a_lo * (w_hi 2^11)        (then out = acc * 2^-11)
 // Every f16 x f16 product is exact in fp32; the dropped a_lo w_lo term and the roundings bound the
 // error per product by ~2^-21 relative (a_lo goes subnormal below |a| ~ 2^-3, adding <= 2^-25
-// absolute), below fp32's own accumulation rounding over K = 9 * Cin terms. Measured on the reduced and full UNet (tests/
-// test_cpu_split_numerics.py emulates this exact arithmetic on CPU): max-abs vs an fp64 UNet is
-// the same as the fp32 UNet's (8.3e-7 vs 9.6e-7 at 256^2). Cost: 3 MFMAs at the f16 rate =
-// 5.3x the fp32 MFMA rate for the same K. The 2^11 weight scale needs |w| < 32 (host-checked;
-// a layer outside that range stays on the fp32 kernel).
+// absolute), below fp32's own accumulation rounding over K = 9 * Cin terms. Measured on the
+// reduced and full UNet (tests/test_cpu_split_numerics.py emulates this exact arithmetic on CPU):
+// max-abs vs an fp64 UNet is the same as the fp32 UNet's (8.7e-7 vs 9.6e-7 at 256^2). Cost: 3
+// MFMAs at the f16 rate = 5.3x the fp32 MFMA rate for the same K. The 2^11 weight scale needs
+// |w| < 32 (host-checked; a layer outside that range stays on the fp32 kernel).
 //
-// Structure (one persistent workgroup per CU; the LDS footprint forces it): the conv_stream.hip
-// design with K-chunks of 16 channels.
+// Structure: one persistent workgroup per CU (the LDS footprint forces it) walks a strided list
+// of work units = (256-pixel tile of one image: 8 x 32 or 16 x 16 pixels, 64-channel tile, K split
+// z); K runs in chunks of 16 channels and the chunk stream continues across units without a break.
+// Low-resolution layers split K over S units so the grid covers the chip; their partial sums go
+// to slabs that splitk_reduce (conv.hip) finishes with bias and residual.
 //   * waves 0-3 consumers (one per SIMD): per tap 4 A-fragment (hi/lo x 2 pixel blocks) and 4
 //     B-fragment ds_read_b128, 12 v_mfma_f32_32x32x16_f16; next tap's fragments pinned after the
-//     first MFMA group; after a tile's last chunk the epilogue straight from the accumulators
+//     first MFMA group; after a unit's last chunk the epilogue straight from the accumulators
 //     (x 2^-11, bias, residual prefetched during the last chunk, GroupNorm granule statistics,
-//     fire-and-forget dword stores that drain behind the next tile).
+//     fire-and-forget dword stores that drain behind the next unit).
 //   * waves 4-7 producers: halo of chunk j+2 in registers (buffer descriptors, no per-chunk VALU
 //     address work), weights of chunk j+2 by LDS-DMA, prologue of chunk j+1 (GroupNorm-apply
 //     [+ scale/shift] + SiLU, nearest-up, zero padding) + the f16 split, LDS writes.
-// LDS: A = 4 planes [part hi/lo][channel half h][340 halo px][8 f16] (21.25 KiB) double-buffered,
+//   * a ResBlock's 1x1 skip segment (the chunks after the 3x3 ones): the producers LDS-DMA the raw
+//     block input into the spare 32 KiB of the chunk's weight-ring slot and the consumers split it
+//     in registers: a 1x1 chunk is too short (12 MFMAs) to hide register-staged loads two chunks
+//     ahead, and the DMA needs no producer registers or VALU.
+// LDS: A = 4 planes [part hi/lo][channel half h][halo px][8 f16] (<= 21.25 KiB) double-buffered,
 // W = [tap][part][h][64 co][8 f16] (36 KiB) in a 3-slot ring (DMA two chunks ahead).
 #include "conv.h"
 #include "conv_dev.h"
@@ -34,8 +41,7 @@
 // Timing-only ablation builds (never shipped; outputs are garbage): X3_ABLATE=
 //   1 producers skip the halo loads and LDS writes (weights DMA + barriers only)
 //   2 producers load the halo but skip the prologue / split / LDS writes
-//   3 consumers skip the MFMAs (fragment reads kept)   4 consumers idle (barriers only)
-//   5 no weight DMA                                    7 producers store without act / split VALU
+//   4 consumers idle (barriers only)      5 no weight DMA
 //   8 producers idle (no DMA, no halo)   9 = 8 + no consumer epilogue   10 = 9 + no barriers
 #ifndef X3_ABLATE
 #define X3_ABLATE 0
@@ -48,49 +54,91 @@ namespace {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) f16x8 lds_h8;
 
-constexpr int XBN = 64, XTW = 32, XTH = 8;
-constexpr int XHW = XTW + 2, XHH = XTH + 2;            // halo 34 x 10
-constexpr int XNP = XHW * XHH;                         // 340 halo pixels
-constexpr int XITEMS = (2 * XNP + NP_T - 1) / NP_T;    // 3 (pixel, channel half) items per producer thread
-constexpr int XA = 4 * XNP * 4;                        // floats per A stage (4 planes x 340 x 16 B)
-constexpr int XW = 9 * 2 * 2 * XBN * 4;                // floats per W stage (36 KiB)
-constexpr int XWDMA = XW / 4 / NP_T;                   // 16-B LDS-DMA rounds per producer thread (9)
-constexpr int X_LDS_FLOATS = 2 * XA + 3 * XW;          // 38528 floats = 150.5 KiB
-constexpr float kLo = 2048.0f;                         // 2^11
+constexpr int XBN = 64;
+constexpr int XNPMAX = 340;                    // halo pixels of the largest tile (8 x 32 -> 10 x 34)
+constexpr int XA = 4 * XNPMAX * 4;             // floats per A stage (4 planes x 340 px x 16 B)
+constexpr int XW = 9 * 2 * 2 * XBN * 4;        // floats per weight-ring slot (36 KiB)
+constexpr int XWDMA = XW / 4 / NP_T;           // 16-B LDS-DMA rounds per producer thread (9)
+constexpr int X_LDS_FLOATS = 2 * XA + 3 * XW;  // 38528 floats = 150.5 KiB
+constexpr int XSKA = 1024;                     // skip chunk slot: weights [0, XSKA), operand planes after
+constexpr float kLo = 2048.0f;                 // 2^11
 static_assert(XW % (4 * NP_T) == 0, "weight slab must be whole DMA rounds");
-
-// LDS-DMA ops and register loads issued per producer interval (the barrier's vmcnt arithmetic)
-constexpr int X_LOADS_PER_CHUNK = 2 * XITEMS + 4;
+static_assert(XSKA + 2 * 4096 <= XW, "skip chunk slot layout");
 
 #define XBARRIER_CONSUMER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #define XBARRIER_PRODUCER(N) asm volatile("s_waitcnt vmcnt(" #N ") lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-template <int XF>
+// Tile of 256 output pixels of one image, TW x TH; halo (TW + 2) x (TH + 2).
+template <int TW>
+struct XGeo {
+  static constexpr int TH = 256 / TW;
+  static constexpr int HW = TW + 2;
+  static constexpr int NP = HW * (TH + 2);                  // 340 (8 x 32), 324 (16 x 16)
+  static constexpr int ITEMS = (2 * NP + NP_T - 1) / NP_T;  // (pixel, channel half) items per producer thread
+  static_assert(NP <= XNPMAX && ITEMS == 3, "halo staging: 3 items per producer thread");
+};
+// Every producer interval issues exactly 9 LDS-DMA ops then 10 register loads (barrier arithmetic).
+constexpr int X_LOADS_PER_CHUNK = 2 * 3 + 4;
+
+// Work unit L -> (tile, split z). The S splits of a tile are consecutive L; pixel tiles in groups
+// of 8 get channel-tile IDs 8 apart (conv.hip's XCD-aware map) when the tile count allows. Every
+// divisor is a power of two (run_conv requires power-of-two sizes; S, cout / 64 in {1, 2, 4, 8}),
+// so the decode is shifts and masks on log2 values taken once per kernel.
+struct XDec {
+  int lks, lnct, ltx, lty;
+  bool xcd;
+};
+__device__ __forceinline__ XDec x3_dec(const ConvParams& p, int nct) {
+  return {__builtin_ctz(p.ksplit), __builtin_ctz(nct), __builtin_ctz(p.tiles_x), __builtin_ctz(p.tiles_y),
+          p.npix_tiles % 8 == 0};
+}
+__device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int L, int& z) {
+  z = L & ((1 << d.lks) - 1);
+  const int v = L >> d.lks;
+  STile t;
+  int bx;
+  if (d.xcd) {
+    const int rr = v & ((8 << d.lnct) - 1);
+    t.ct = rr >> 3;
+    bx = ((v >> (3 + d.lnct)) << 3) + (rr & 7);
+  } else {
+    t.ct = v & ((1 << d.lnct) - 1);
+    bx = v >> d.lnct;
+  }
+  t.x0 = (bx & ((1 << d.ltx) - 1)) * p.TW;
+  bx >>= d.ltx;
+  t.y0 = (bx & ((1 << d.lty) - 1)) * p.TH;
+  t.n0 = bx >> d.lty;
+  return t;
+}
+
 struct XSet {
-  f32x4 raw[XITEMS][2];
+  f32x4 raw[3][2];
   f32x4 ca[2], cb[2];
-  float vld[XITEMS];
+  float vld[3];
 };
 
-template <int XF, bool SKIP>
+template <int XF, bool SKIP, int TW>
 struct XProducer {
+  using Geo = XGeo<TW>;
   int ptid, hh;  // hh: channel half (8 of the chunk's 16 channels) this thread stages
-  int hy[XITEMS], hx[XITEMS], ldso[XITEMS];  // ldso: 16-B slot of the pixel in the hi plane; -1 unused
-  int cur_tile = -1;
+  int hy[3], hx[3], ldso[3];  // ldso: 16-B slot of the pixel in the hi plane; -1 unused
+  int cur_unit = -1;
   rsrc_t r0, r1, ra, rb;
-  int off0[XITEMS], off1[XITEMS], so[XITEMS];  // so: output-resolution pixel (skip segment)
+  int off0[3], off1[3];
   int tn0;
-  float valid[XITEMS];
+  int skp[4];  // skip segment: image pixel of tile pixel 64 i + lane
+  float valid[3];
 
   __device__ __forceinline__ void init(int t) {
     ptid = t;
     hh = t & 1;
 #pragma unroll
-    for (int i = 0; i < XITEMS; ++i) {
+    for (int i = 0; i < 3; ++i) {
       const int idx = t + i * NP_T, pix = idx >> 1;
-      hy[i] = pix / XHW;
-      hx[i] = pix - hy[i] * XHW;
-      ldso[i] = idx < 2 * XNP ? hh * XNP + pix : -1;
+      hy[i] = pix / Geo::HW;
+      hx[i] = pix - hy[i] * Geo::HW;
+      ldso[i] = idx < 2 * Geo::NP ? hh * Geo::NP + pix : -1;
     }
   }
 
@@ -103,61 +151,63 @@ struct XProducer {
     ra = p.actA ? mkrsrc(p.actA + (size_t)t.n0 * ctot) : r0;
     rb = p.actB ? mkrsrc(p.actB + (size_t)t.n0 * ctot) : r0;
     tn0 = t.n0;
+    if (SKIP) {
 #pragma unroll
-    for (int i = 0; i < XITEMS; ++i) {
+      for (int i = 0; i < 4; ++i) {
+        const int m = 64 * i + (ptid & 63);
+        skp[i] = (t.y0 + m / TW) * p.W + t.x0 + m % TW;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
       const int y = t.y0 + hy[i] - 1, x = t.x0 + hx[i] - 1;
       const bool inb = ldso[i] >= 0 && y >= 0 && y < p.H && x >= 0 && x < p.W;
       int sy = y, sx = x;
       if (XF == XF_UP) { sy = y >> 1; sx = x >> 1; }
       const int sp = inb ? sy * p.Win + sx : 0;
-      so[i] = inb ? y * p.W + x : 0;
       valid[i] = inb ? 1.f : 0.f;
       off0[i] = (sp * p.c0 + 8 * hh) * 4;
       off1[i] = (sp * p.c1 + 8 * hh) * 4;
     }
   }
 
-  // Global loads of chunk k (16 channels) of tile t into set s; chunks >= nmain belong to the 1x1
-  // skip segment. Exactly X_LOADS_PER_CHUNK loads on every path (see conv_stream.hip
-  // SProducer::load for why).
-  __device__ __forceinline__ void load(XSet<XF>& s, const ConvParams& p, const STile& t, int ti, int k, int nmain) {
-    if (ti != cur_tile) {
+  // Global loads of chunk c (16 channels; c >= nmain: the 1x1 skip segment) of the entered unit
+  // into set s: exactly X_LOADS_PER_CHUNK loads on every path (see conv_stream.hip SProducer::load).
+  // per-unit state (descriptors, pixel offsets): before the unit's first DMA or load
+  __device__ __forceinline__ void enter(const ConvParams& p, const STile& t, int u) {
+    if (u != cur_unit) {
       tile_setup(p, t);
-      cur_tile = ti;
+      cur_unit = u;
     }
-    const int cb0 = 16 * k;
+  }
+
+  __device__ __forceinline__ void load(XSet& s, const ConvParams& p, int c, int nmain) {
 #pragma unroll
-    for (int i = 0; i < XITEMS; ++i) s.vld[i] = valid[i];
+    for (int i = 0; i < 3; ++i) s.vld[i] = valid[i];
     if (X3_ABLATE == 1 || X3_ABLATE >= 8) return;
-    if (SKIP && k >= nmain) {
-      // 1x1 skip segment: raw block input at output resolution (the consumer reads only the
-      // centre tap, i.e. the tile's own pixels; the halo ring loads are unused)
-      const int cs = 16 * (k - nmain);
-      const bool first = cs < p.sc0;
-      const int sc = first ? p.sc0 : p.sc1;
-      const rsrc_t rs = mkrsrc((first ? p.s0 : p.s1) + (size_t)tn0 * p.H * p.W * sc);
-      const int cso = (first ? cs : cs - p.sc0) * 4;
+    if (SKIP && c >= nmain) {
+      // the skip chunk's operand arrives by LDS-DMA (dma); these only keep the count (one line)
 #pragma unroll
-      for (int i = 0; i < XITEMS; ++i) {
-        const int o = (so[i] * sc + 8 * hh) * 4;
-        s.raw[i][0] = bld4(rs, o, cso);
-        s.raw[i][1] = bld4(rs, o + 16, cso);
+      for (int i = 0; i < 3; ++i) {
+        s.raw[i][0] = bld4(r0, 0, 0);
+        s.raw[i][1] = bld4(r0, 0, 0);
       }
-      s.ca[0] = bld4(ra, 0, 0);  // unused (act NONE): keeps the per-chunk load count fixed
+      s.ca[0] = bld4(ra, 0, 0);
       s.ca[1] = bld4(ra, 0, 0);
       s.cb[0] = bld4(rb, 0, 0);
       s.cb[1] = bld4(rb, 0, 0);
       return;
     }
+    const int cb0 = 16 * c;
     if (cb0 < p.c0) {
 #pragma unroll
-      for (int i = 0; i < XITEMS; ++i) {
+      for (int i = 0; i < 3; ++i) {
         s.raw[i][0] = bld4(r0, off0[i], cb0 * 4);
         s.raw[i][1] = bld4(r0, off0[i] + 16, cb0 * 4);
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < XITEMS; ++i) {
+      for (int i = 0; i < 3; ++i) {
         s.raw[i][0] = bld4(r1, off1[i], (cb0 - p.c0) * 4);
         s.raw[i][1] = bld4(r1, off1[i] + 16, (cb0 - p.c0) * 4);
       }
@@ -168,20 +218,34 @@ struct XProducer {
     s.cb[1] = bld4(rb, 32 * hh + 16, cb0 * 4);
   }
 
-  // Weight slab of chunk k of channel tile ct into W stage `Wslot` by LDS-DMA: 9 rounds of 1 KiB
-  // per producer wave for a 3x3 chunk, 1 round for a 1x1 skip chunk ([1 tap][part][h][64][8]).
-  __device__ __forceinline__ void dma_weights(const ConvParams& p, int ct, int k, int nmain, int nskip,
-                                              lds_f* Wslot) const {
+  // LDS-DMA of chunk c of channel tile ct into ring slot `Wslot`, always XWDMA ops per thread:
+  //   3x3 chunk: the weight slab (9 rounds of 1 KiB per producer wave);
+  //   skip chunk kk: weights [1][part][h][64][8] (4 KiB, one round) at slot offset 0; the raw fp32
+  //     operand (16 channels of the tile's 256 pixels, from s0 or s1) as 4 quad planes
+  //     [h][q][256 px][4 fp32] at XSKA (wave pw copies plane pw in 4 rounds; the consumer splits
+  //     it in registers); then 4 filler rounds into the slot's tail.
+  __device__ __forceinline__ void dma(const ConvParams& p, int ct, int c, int nmain, int nskip, lds_f* Wslot) const {
     if (X3_ABLATE == 5 || X3_ABLATE >= 8) return;
     const int pw = __builtin_amdgcn_readfirstlane(ptid >> 6);
-    if (SKIP && k >= nmain) {
-      const rsrc_t r = mkrsrc(p.wskip + ((size_t)ct * nskip + (k - nmain)) * (XW / 9));
+    if (SKIP && c >= nmain) {
+      const int kk = c - nmain;
+      const rsrc_t r = mkrsrc(p.wskip + ((size_t)ct * nskip + kk) * (XW / 9));
       const int qb = pw * 64;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(Wslot + 4 * qb), 16,
                                                16 * (qb + (ptid & 63)), 0, 0, 0);
+      const int cs = 16 * kk;
+      const bool first = cs < p.sc0;
+      const int sc = first ? p.sc0 : p.sc1;
+      const rsrc_t rs = mkrsrc((first ? p.s0 : p.s1) + (size_t)tn0 * p.H * p.W * sc);
+      const int soff = ((first ? cs : cs - p.sc0) + 8 * (pw >> 1) + 4 * (pw & 1)) * 4;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(Wslot + XSKA + 4096 * (i >> 2) + pw * 1024 + 256 * (i & 3)),
+            16, skp[i & 3] * sc * 4, soff, 0, 0);
       return;
     }
-    const rsrc_t r = mkrsrc(p.wpack + ((size_t)ct * nmain + k) * XW);
+    const rsrc_t r = mkrsrc(p.wpack + ((size_t)ct * nmain + c) * XW);
 #pragma unroll
     for (int i = 0; i < XWDMA; ++i) {
       const int qb = (i * 4 + pw) * 64;
@@ -201,20 +265,11 @@ struct XProducer {
   }
 
   // prologue + split: hi plane at slot ldso, lo plane 2 planes further
-  __device__ __forceinline__ void store(const XSet<XF>& s, int act, lds_f* As) const {
+  __device__ __forceinline__ void store(const XSet& s, int act, lds_f* As) const {
     if (X3_ABLATE == 1 || X3_ABLATE == 2 || X3_ABLATE >= 8) return;
 #pragma unroll
-    for (int i = 0; i < XITEMS; ++i) {
-      if (X3_ABLATE == 7 && ldso[i] >= 0) {
-        f16x8 h8;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          h8[j] = (_Float16)s.raw[i][0][j];
-          h8[4 + j] = (_Float16)s.raw[i][1][j];
-        }
-        *(lds_h8*)(As + 4 * ldso[i]) = h8;
-        *(lds_h8*)(As + 4 * (ldso[i] + 2 * XNP)) = h8;
-      } else if (ldso[i] >= 0) {
+    for (int i = 0; i < 3; ++i) {
+      if (ldso[i] >= 0) {
         f16x8 h8, l8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -225,31 +280,28 @@ struct XProducer {
           l8[j] = (_Float16)(v - (float)hv);  // exact difference, rounded once
         }
         *(lds_h8*)(As + 4 * ldso[i]) = h8;
-        *(lds_h8*)(As + 4 * (ldso[i] + 2 * XNP)) = l8;
+        *(lds_h8*)(As + 4 * (ldso[i] + 2 * Geo::NP)) = l8;
       }
     }
   }
 };
 
-// MFMAs over one staged chunk: TAPS taps x (3 split products x 2 x 2 fragment blocks). TAPS = 1
-// is the skip segment's 1x1 chunk: centre tap of the halo layout, weight slab [1][part][h][64][8].
 __device__ __forceinline__ f32x16 xmfma(f16x8 a, f16x8 b, f32x16 c) {
-  if (X3_ABLATE == 3) {
-    asm volatile("" : "+v"(c) : "v"(a), "v"(b));
-    return c;
-  }
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-template <int TAPS>
+// MFMAs over one staged 3x3 chunk: 9 taps x (3 split products x 2 x 2 fragment blocks);
+// operand = the halo stage (planes of Geo::NP pixels, pb = halo pixel).
+template <int TW>
 __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws, const int (&pb)[2]) {
+  using Geo = XGeo<TW>;
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-  const lds_f* Ah = As + 4 * (h * XNP);
-  const lds_f* Al = As + 4 * ((2 + h) * XNP);
+  const lds_f* Ah = As + 4 * (h * Geo::NP);
+  const lds_f* Al = As + 4 * ((2 + h) * Geo::NP);
   const lds_f* Wb = Ws + 4 * (h * XBN + l32);
   f16x8 ah[2][2], al[2][2], bs[2][2], bl[2][2];
   auto fetch = [&](int tap, int slot) {
-    const int toff = TAPS == 9 ? (tap / 3) * XHW + (tap % 3) : XHW + 1;
+    const int toff = (tap / 3) * Geo::HW + (tap % 3);
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr) {
       ah[slot][mr] = *(const lds_h8*)(Ah + 4 * (pb[mr] + toff));
@@ -263,7 +315,7 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
   };
   fetch(0, 0);
 #pragma unroll
-  for (int tap = 0; tap < TAPS; ++tap) {
+  for (int tap = 0; tap < 9; ++tap) {
     const int cur = tap & 1;
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr)
@@ -271,7 +323,7 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
       for (int nr = 0; nr < 2; ++nr)
         acc[mr][nr] = xmfma(ah[cur][mr], bs[cur][nr], acc[mr][nr]);
     __builtin_amdgcn_sched_barrier(0);
-    if (tap + 1 < TAPS) fetch(tap + 1, cur ^ 1);
+    if (tap + 1 < 9) fetch(tap + 1, cur ^ 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr)
@@ -287,34 +339,78 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
   }
 }
 
-template <int XF, bool SKIP>
+// One 1x1 skip chunk: the raw fp32 operand (quad planes [h][q][256 px][4] at As) is split in
+// registers with the producers' arithmetic (a_hi = f16(a), a_lo = f16(a - a_hi)), then the 3
+// split products x 2 x 2 fragment blocks. pb = tile pixel.
+__device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws,
+                                             const int (&pb)[2]) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+  const lds_f* Wb = Ws + 4 * (h * XBN + l32);
+  f16x8 ah[2], al[2], bs[2], bl[2];
+#pragma unroll
+  for (int mr = 0; mr < 2; ++mr) {
+    const f32x4 q0 = *(const lds_f4*)(As + 4 * ((2 * h) * 256 + pb[mr]));
+    const f32x4 q1 = *(const lds_f4*)(As + 4 * ((2 * h + 1) * 256 + pb[mr]));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = j < 4 ? q0[j] : q1[j - 4];
+      const _Float16 hv = (_Float16)v;
+      ah[mr][j] = hv;
+      al[mr][j] = (_Float16)(v - (float)hv);
+    }
+  }
+#pragma unroll
+  for (int nr = 0; nr < 2; ++nr) {
+    bs[nr] = *(const lds_h8*)(Wb + 4 * (nr * 32));
+    bl[nr] = *(const lds_h8*)(Wb + 4 * (2 * XBN + nr * 32));
+  }
+#pragma unroll
+  for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+    for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(ah[mr], bs[nr], acc[mr][nr]);
+#pragma unroll
+  for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+    for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(ah[mr], bl[nr], acc[mr][nr]);
+#pragma unroll
+  for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+    for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(al[mr], bs[nr], acc[mr][nr]);
+}
+
+template <int XF, bool SKIP, int TW>
 __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
+  using Geo = XGeo<TW>;
   extern __shared__ __attribute__((aligned(16))) float smem_raw[];
   lds_f* const smem = (lds_f*)(smem_raw);
-  lds_f* const A0 = smem;                 // stage s at A0 + s * XA
-  lds_f* const W0 = smem + 2 * XA;        // ring slot s at W0 + s * XW
+  lds_f* const A0 = smem;           // stage s at A0 + s * XA
+  lds_f* const W0 = smem + 2 * XA;  // ring slot s at W0 + s * XW
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool consumer = __builtin_amdgcn_readfirstlane(wave) < 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool consumer = wave < 4;
   const int nct = p.cout_pad / XBN;
-  const int nvirt = p.npix_tiles * nct;
+  const int S = p.ksplit;
+  const int nunit = p.npix_tiles * nct * S;
   const int G = gridDim.x;
-  const int ntile = (nvirt - (int)blockIdx.x + G - 1) / G;  // host guarantees >= 1
+  const int nu = (nunit - (int)blockIdx.x + G - 1) / G;  // host guarantees >= 1
   const int nmain = p.cin_pad / 16;
   const int nskip = SKIP ? p.cs_pad / 16 : 0;
-  const int nch = nmain + nskip;  // chunks per tile: 3x3 segment, then the 1x1 skip segment
-  const int J = ntile * nch;
-  auto tile_of = [&](int ti) { return decode_tile(p, (int)blockIdx.x + ti * G, nct); };
+  const int nchu = (nmain + nskip) / S;  // chunks per unit (host: divisible)
+  const int J = nu * nchu;
+  const XDec dec = x3_dec(p, nct);
+  auto unit_of = [&](int u, int& z) { return x3_unit(p, dec, (int)blockIdx.x + u * G, z); };
 
   if (consumer) {
     const int h = lane >> 5, l32 = lane & 31;
     const int wm0 = wave * 64;
     f32x16 acc[2][2];
-    int pb[2];
+    int pb[2], pbs[2];
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr) {
       const int m = wm0 + mr * 32 + l32;
-      pb[mr] = (m >> 5) * XHW + (m & 31);
+      pb[mr] = (m / TW) * Geo::HW + (m % TW);
+      pbs[mr] = m;
     }
     auto zero = [&]() {
 #pragma unroll
@@ -324,29 +420,39 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[mr][nr][r] = 0.f;
     };
-    // Epilogue straight from the accumulators. Lane (h, l32) holds channel 32 nr + l32 of pixels
-    // (row 2 wave + mr, column (r & 3) + 8 (r >> 2) + 4 h) of the 8 x 32 tile: one dword store per
-    // register = two 128-B row segments. Bias and residual are loaded in the same layout while the
-    // tile's last chunk is on the MFMAs, so the epilogue waits on nothing and its stores drain
-    // behind the next tile's chunks.
+    // Epilogue straight from the accumulators. Lane (h, l32) holds channel 32 nr + l32 of tile
+    // pixel wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3) (column offset 4 h + (r & 3) < 8 stays in
+    // its row): one dword store per register = two 128-B row segments. Bias and residual are
+    // loaded in the same layout while the unit's last chunk is on the MFMAs, so the epilogue
+    // waits on nothing and its stores drain behind the next unit's chunks.
     float rv[2][2][16];
     float bias2[2];
-    auto col_soff = [&](int r) { return ((r & 3) + 8 * (r >> 2)) * p.cout * 4; };  // wave-uniform
+    // Register (mr, r) of lane (h, l32) sits at tile pixel wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3).
+    // Byte offsets: vbase (lane: tile origin, the wave's rows, 4 h, channel) + mr * mstep (lane) +
+    // roff(r) (16 wave-uniform scalar offsets).
+    auto roff = [&](int r) {
+      const int lin = 8 * (r >> 2) + (r & 3);
+      return ((lin / TW) * p.W + lin % TW) * p.cout * 4;
+    };
+    const int mstep = (32 / TW) * p.W * p.cout * 4;
+    auto vbase = [&](const STile& t) {
+      return (((t.y0 + wm0 / TW) * p.W + t.x0 + 4 * h) * p.cout + t.ct * XBN + l32) * 4;
+    };
     auto prefetch = [&](const STile& t) {
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr) bias2[nr] = gld1(p.bias + t.ct * XBN + 32 * nr + l32);
       if (!p.res) return;
       const rsrc_t rr = mkrsrc(p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout);
       if (p.res_xform == XF_NONE) {
-        const int vb = (((t.y0 + 2 * wave) * p.W + t.x0 + 4 * h) * p.cout + t.ct * XBN + l32) * 4;
+        const int vb = vbase(t);
 #pragma unroll
         for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
           for (int nr = 0; nr < 2; ++nr)
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-              rv[mr][nr][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                            rr, vb + mr * p.W * p.cout * 4 + nr * 128, col_soff(r), 0));
+              rv[mr][nr][r] = __builtin_bit_cast(
+                  float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb + mr * mstep + nr * 128, roff(r), 0));
       } else {  // XF_UP: nearest-upsampled residual (XF_DOWN residuals arrive pre-pooled)
 #pragma unroll
         for (int mr = 0; mr < 2; ++mr)
@@ -354,15 +460,29 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           for (int nr = 0; nr < 2; ++nr)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int y = (t.y0 + 2 * wave + mr) >> 1, x = (t.x0 + 4 * h + (r & 3) + 8 * (r >> 2)) >> 1;
+              const int lin = wm0 + 32 * mr + 8 * (r >> 2) + 4 * h + (r & 3);
+              const int y = (t.y0 + lin / TW) >> 1, x = (t.x0 + lin % TW) >> 1;
               const int o = ((y * p.res_W + x) * p.cout + t.ct * XBN + 32 * nr + l32) * 4;
               rv[mr][nr][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, o, 0, 0));
             }
       }
     };
-    auto epilogue = [&](const STile& t) {
-      const rsrc_t ro = mkrsrc(p.out + (size_t)t.n0 * p.H * p.W * p.cout);
-      const int vb = (((t.y0 + 2 * wave) * p.W + t.x0 + 4 * h) * p.cout + t.ct * XBN + l32) * 4;
+    auto epilogue = [&](const STile& t, int z) {
+      const size_t img = (size_t)p.H * p.W * p.cout;
+      const int vb = vbase(t);
+      if (S > 1) {  // raw partial sums into slab z (splitk_reduce adds the slabs, bias, residual)
+        const rsrc_t rp = mkrsrc(p.part + ((size_t)z * p.N + t.n0) * img);
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+          for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[mr][nr][r] * (1.0f / kLo)), rp,
+                                                    vb + mr * mstep + nr * 128, roff(r), 0);
+        return;
+      }
+      const rsrc_t ro = mkrsrc(p.out + (size_t)t.n0 * img);
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr) {
         float v[2][16];
@@ -374,8 +494,8 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
             x = x + bias2[nr];
             if (p.res) x = rv[mr][nr][r] + x;  // torch order: x_res + (conv + bias)
             v[mr][r] = x;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro,
-                                                  vb + mr * p.W * p.cout * 4 + nr * 128, col_soff(r), 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep + nr * 128,
+                                                  roff(r), 0);
           }
         if (p.gstat) {
           // GroupNorm granule statistics: channel over this lane's 32 pixels (two-pass), merged
@@ -406,7 +526,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           g = xmerge(g, 1);
           g = xmerge(g, 2);
           if (h == 0 && (l32 & 3) == 0) {
-            const int e = ((t.y0 / XTH) * p.tiles_x + t.x0 / XTW) * 4 + wave;
+            const int e = ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
             float* o = p.gstat + (((size_t)t.n0 * p.gstat_E + e) * (p.cout / 4) + t.ct * 16 + nr * 8 + (l32 >> 2)) * 2;
             o[0] = g.mean;
             o[1] = g.m2;
@@ -416,86 +536,88 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     };
     zero();
     XBARRIER_CONSUMER();  // chunk 0 staged
-    int k = 0, ti = 0;
+    int kk = 0, u = 0, z = 0;
+    STile t = unit_of(0, z);
     for (int j = 0; j < J; ++j) {
       const lds_f* Ws = W0 + (j % 3) * XW;
-      if (k == nch - 1 && X3_ABLATE < 9) prefetch(tile_of(ti));
+      const int c = z * nchu + kk;  // chunk index within the tile's K stream
+      if (kk == nchu - 1 && S == 1 && X3_ABLATE < 9) prefetch(t);
       if (X3_ABLATE == 4) {
-      } else if (!SKIP || k < nmain) {
-        consume_x3<9>(acc, A0 + (j & 1) * XA, Ws, pb);
+      } else if (!SKIP || c < nmain) {
+        consume_x3<TW>(acc, A0 + (j & 1) * XA, Ws, pb);
       } else {
-        consume_x3<1>(acc, A0 + (j & 1) * XA, Ws, pb);
+        consume_skip(acc, Ws + XSKA, Ws, pbs);
       }
-      if (++k == nch) {
-        k = 0;
+      if (++kk == nchu) {
+        kk = 0;
         if (X3_ABLATE < 9)
-          epilogue(tile_of(ti));
+          epilogue(t, z);
         else
           asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
-        ++ti;
         zero();
+        if (++u < nu) t = unit_of(u, z);
       }
       if (X3_ABLATE != 10) XBARRIER_CONSUMER();
     }
     return;
   }
 
-  // ---- producers: halo two chunks ahead in registers, weights two chunks ahead by LDS-DMA into
-  // a 3-slot ring (chunk c in slot c % 3) ----
+  // ---- producers: halo two chunks ahead in registers, weights (and skip operands) two chunks
+  // ahead by LDS-DMA into a 3-slot ring (chunk j in slot j % 3) ----
   const int ptid = tid - NP_T;
-  XProducer<XF, SKIP> P;
+  XProducer<XF, SKIP, TW> P;
   P.init(ptid);
-  XSet<XF> s0, s1;
-  auto load_chunk = [&](XSet<XF>& s, int c) {
-    c = min(c, J - 1);
-    const int ti = c / nch, kk = c - ti * nch;
-    P.load(s, p, tile_of(ti), ti, kk, nmain);
+  XSet s0, s1;
+  // Lookahead cursor over the chunk stream: position jl = (unit ul, chunk kl of the unit), the
+  // unit's tile decoded once per unit; past the end it stays on the last chunk (re-issued loads /
+  // DMA of identical bytes keep the op counts fixed). mainq[q & 1]: chunk q is a 3x3 chunk.
+  int jl = 0, ul = 0, kl = 0, zl = 0;
+  STile tl = unit_of(0, zl);
+  bool mainq[2] = {true, true};
+  auto issue = [&](XSet& s) {  // DMA + register loads of the cursor's chunk, then advance
+    const int c = zl * nchu + kl;
+    mainq[jl & 1] = !SKIP || c < nmain;
+    P.enter(p, tl, ul);
+    P.dma(p, tl.ct, c, nmain, nskip, W0 + (jl % 3) * XW);
+    P.load(s, p, c, nmain);
+    if (jl + 1 < J) {
+      ++jl;
+      if (++kl == nchu) {
+        kl = 0;
+        tl = unit_of(++ul, zl);
+      }
+    } else {
+      jl += 3;  // parity / ring slot of the clamped repeats: keep writing slot (J - 1) % 3
+    }
   };
-  // prologue of chunk c: the main segment's activation, none for the skip segment
-  auto act_of = [&](int c) { return !SKIP || (c % nch) < nmain ? p.act : (int)ACT_NONE; };
-  auto dma_chunk = [&](int c) {
-    c = min(c, J - 1);  // past the end: re-copies the last chunk's identical bytes
-    const int ti = c / nch, kk = c - ti * nch;
-    P.dma_weights(p, tile_of(ti).ct, kk, nmain, nskip, W0 + (c % 3) * XW);
-  };
-  dma_chunk(0);
-  dma_chunk(1);
-  load_chunk(s0, 0);
-  load_chunk(s1, 1);
-  P.store(s0, act_of(0), A0);  // waits for chunk 0's loads, hence for both older DMAs
+  issue(s0);  // chunk 0
+  issue(s1);  // chunk 1
+  P.store(s0, p.act, A0);  // chunk 0 is a 3x3 chunk; waits for its loads, hence its DMA
   XBARRIER_PRODUCER(10);
-  static_assert(X_LOADS_PER_CHUNK == 10, "barrier vmcnt literals");
-  // interval j: weights of chunk j+2 (DMA), halo of chunk j+2, LDS writes of chunk j+1, barrier
-  // once chunk j+1's DMA (issued in interval j-1) has landed: younger than it are the 10 halo
-  // loads of chunk j+1, the DMA of chunk j+2 (9 ops; 1 for a skip chunk) and its 10 halo loads
-#define X3_PRODUCER_BARRIER()            \
-  do {                                   \
-    if constexpr (SKIP)                  \
-      XBARRIER_PRODUCER(21);             \
-    else                                 \
-      XBARRIER_PRODUCER(29);             \
-  } while (0)
+  static_assert(X_LOADS_PER_CHUNK == 10 && XWDMA == 9, "barrier vmcnt literals");
   if (X3_ABLATE == 10) return;
+  // interval j: DMA of chunk j+2 (9 ops), halo loads of chunk j+2 (10), LDS writes of chunk j+1,
+  // then the barrier once chunk j+1's DMA (issued in interval j-1) has landed: younger than it
+  // are chunk j+1's 10 loads, chunk j+2's 9 DMA ops and its 10 loads -> vmcnt(29)
   for (int j = 0; j < J; j += 2) {
-    dma_chunk(j + 2);
-    load_chunk(s0, j + 2);
-    if (j + 1 < J) P.store(s1, act_of(j + 1), A0 + XA);
-    X3_PRODUCER_BARRIER();
+    const bool m1 = mainq[(j + 1) & 1];
+    issue(s0);  // chunk j+2
+    if (j + 1 < J && m1) P.store(s1, p.act, A0 + XA);
+    XBARRIER_PRODUCER(29);
     if (j + 1 >= J) break;
-    dma_chunk(j + 3);
-    load_chunk(s1, j + 3);
-    if (j + 2 < J) P.store(s0, act_of(j + 2), A0);
-    X3_PRODUCER_BARRIER();
+    const bool m2 = mainq[(j + 2) & 1];
+    issue(s1);  // chunk j+3
+    if (j + 2 < J && m2) P.store(s0, p.act, A0);
+    XBARRIER_PRODUCER(29);
   }
-#undef X3_PRODUCER_BARRIER
 }
 
-template <int XF, bool SKIP>
+template <int XF, bool SKIP, int TW>
 static int launch_x3_inst(const ConvParams& p, hipStream_t stream) {
   static bool attr_set = false;
   const size_t lds = (size_t)X_LDS_FLOATS * sizeof(float);
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<XF, SKIP>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<XF, SKIP, TW>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
@@ -507,33 +629,41 @@ static int launch_x3_inst(const ConvParams& p, hipStream_t stream) {
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
   }
-  const int nvirt = p.npix_tiles * (p.cout_pad / XBN);
-  const int grid = nvirt < ncu ? nvirt : ncu;  // one workgroup per CU (LDS-bound)
-  hipLaunchKernelGGL((conv_x3_kernel<XF, SKIP>), dim3(grid), dim3(NT), lds, stream, p);
+  const int nunit = p.npix_tiles * (p.cout_pad / XBN) * p.ksplit;
+  const int grid = nunit < ncu ? nunit : ncu;  // one workgroup per CU (LDS-bound)
+  hipLaunchKernelGGL((conv_x3_kernel<XF, SKIP, TW>), dim3(grid), dim3(NT), lds, stream, p);
   return (int)hipGetLastError();
+}
+
+template <int TW>
+static int launch_x3_tw(const ConvParams& p, int xform, hipStream_t stream) {
+  if (p.wskip) {
+    if (xform == XF_NONE) return launch_x3_inst<XF_NONE, true, TW>(p, stream);
+    return (int)hipErrorInvalidValue;  // the skip segment comes with XF_NONE only (ResBlock conv2)
+  }
+  if (xform == XF_NONE) return launch_x3_inst<XF_NONE, false, TW>(p, stream);
+  if (xform == XF_UP) return launch_x3_inst<XF_UP, false, TW>(p, stream);
+  return (int)hipErrorInvalidValue;
 }
 
 }  // namespace
 
-// Eligible: 3x3, BN = 64, BM = 256 geometry (8 x 32 tiles of one image, whole groups of 8 pixel
-// tiles so the XCD map is a bijection), NHWC epilogue without split-K, cout a multiple of 64,
-// 16-channel chunks on every source (main and skip), no avg-pool prologue (run_conv feeds those
-// layers a pooled activation instead) nor avg-pool residual (pooled likewise). Any act, identity
-// or nearest-up residual, 1x1 skip segment.
+// Eligible: 3x3, BN = 64, 256-pixel tiles of one image (8 x 32 or 16 x 16), NHWC epilogue, cout a
+// multiple of 64, 16-channel chunks on every source (main and skip), K chunks divisible by the
+// split, no avg-pool prologue (run_conv feeds those layers a pooled activation instead) nor
+// avg-pool residual without split-K (pooled likewise). Any act, identity or nearest-up residual,
+// 1x1 skip segment.
 bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
-  return taps == 9 && xform != XF_DOWN && bn == XBN && p.bm == 256 && p.TW == XTW && p.TH == XTH && p.IMGS == 1 &&
-         p.epi == EPI_NHWC && p.ksplit == 1 && p.cout % XBN == 0 && p.cout_pad == p.cout && p.npix_tiles % 8 == 0 &&
+  const int nch = p.cin_pad / 16 + (p.wskip ? p.cs_pad / 16 : 0);
+  return taps == 9 && xform != XF_DOWN && bn == XBN && p.bm == 256 && (p.TW == 32 || p.TW == 16) &&
+         p.TH * p.TW == 256 && p.IMGS == 1 && p.epi == EPI_NHWC && p.cout % XBN == 0 && p.cout_pad == p.cout &&
          p.c0 % 16 == 0 && p.c1 % 16 == 0 && (!p.wskip || (p.sc0 % 16 == 0 && p.sc1 % 16 == 0)) &&
-         (!p.res || p.res_xform != XF_DOWN);
+         p.ksplit >= 1 && nch % p.ksplit == 0 && (!p.res || p.res_xform != XF_DOWN || p.ksplit > 1);
 }
 
 int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream) {
-  if (p.wskip) {
-    if (xform == XF_NONE) return launch_x3_inst<XF_NONE, true>(p, stream);
-    return (int)hipErrorInvalidValue;  // the skip segment comes with XF_NONE only (ResBlock conv2)
-  }
-  if (xform == XF_NONE) return launch_x3_inst<XF_NONE, false>(p, stream);
-  if (xform == XF_UP) return launch_x3_inst<XF_UP, false>(p, stream);
+  if (p.TW == 32) return launch_x3_tw<32>(p, xform, stream);
+  if (p.TW == 16) return launch_x3_tw<16>(p, xform, stream);
   return (int)hipErrorInvalidValue;
 }
 

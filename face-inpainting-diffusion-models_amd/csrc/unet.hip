@@ -490,11 +490,14 @@ int Model::ensure_workspace(int B) {
   // split-K slabs: worst case over every conv of the plan at this batch
   split_floats_ = 0;
   auto consider = [&](const ConvW& cw, int H) {
-    ConvParams g;
-    std::memset(&g, 0, sizeof(g));
-    g.cout_pad = cw.cout_pad;
-    conv_geometry(g, H, H, B, cw.bn, cw.cin_pad / 8);
-    if (g.ksplit > 1) split_floats_ = std::max(split_floats_, (size_t)g.ksplit * B * H * H * cw.cout);
+    for (int x3 = 0; x3 < 2; ++x3) {  // fp32 kernels' geometry and the split kernel's
+      ConvParams g;
+      std::memset(&g, 0, sizeof(g));
+      g.cout_pad = cw.cout_pad;
+      const int nch = x3 ? (cw.cin_pad + (cw.has_skip ? cw.cs_pad : 0)) / 16 : cw.cin_pad / 8;
+      conv_geometry(g, H, H, B, cw.bn, nch, x3 == 1);
+      if (g.ksplit > 1) split_floats_ = std::max(split_floats_, (size_t)g.ksplit * B * H * H * cw.cout);
+    }
   };
   for (auto& r : res_) {
     for (int H = 2; H <= R; H *= 2) {  // resolution is not stored per ResBlock: bound over all sizes
@@ -560,9 +563,10 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   p.out = out;
   p.epi = epi;
   IFD_REQUIRE((H & (H - 1)) == 0, "spatial size must be a power of two");
-  // the persistent split kernel takes 256-pixel tiles whatever the grid (no split-K)
+  // the persistent split kernel: 256-pixel tiles, K split over units at low resolution
   const bool x3_geo = prec_ == IFD_PREC_3XF16 && cw.x3_ok && epi == EPI_NHWC;
-  conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8, x3_geo);
+  const int x3_chunks = (cw.cin_pad + (cw.has_skip ? cw.cs_pad : 0)) / 16;
+  conv_geometry(p, H, H, N, cw.bn, x3_geo ? x3_chunks : cw.cin_pad / 8, x3_geo);
   if (epi != EPI_NHWC) p.ksplit = 1;
   p.part = ws_ + o_split_;
   IFD_REQUIRE(p.ksplit == 1 || (size_t)p.ksplit * N * H * H * cw.cout <= split_floats_, "split-K workspace");
@@ -606,7 +610,10 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
       }
     }
   }
-  const bool use_x3 = prec_ == IFD_PREC_3XF16 && cw.x3_ok && conv_x3_eligible(p, cw.taps, xf, cw.bn);
+  // development switches (bisecting): IFD_X3_OFF=mask: 1 no 16x16 tiles, 2 no split-K, 4 no skip layers
+  static const int x3_off = getenv("IFD_X3_OFF") ? atoi(getenv("IFD_X3_OFF")) : 0;
+  const bool x3_masked = ((x3_off & 1) && p.TW == 16) || ((x3_off & 2) && p.ksplit > 1) || ((x3_off & 4) && cw.has_skip);
+  const bool use_x3 = prec_ == IFD_PREC_3XF16 && cw.x3_ok && !x3_masked && conv_x3_eligible(p, cw.taps, xf, cw.bn);
   if (use_x3) {
     p.wpack = wblob_ + cw.x3_off;
     if (cw.has_skip) p.wskip = wblob_ + cw.x3s_off;
@@ -690,7 +697,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                use_x3 ? "conv_x3" : (use_stream ? "conv_stream" : "conv_kernel"), p.bm,
                cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
     else if (use_x3)
-      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s>", xf, cw.has_skip ? "true" : "false");
+      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d>", xf, cw.has_skip ? "true" : "false", p.TW);
     else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
       snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
     else if (use_stream)
