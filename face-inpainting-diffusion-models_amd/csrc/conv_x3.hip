@@ -43,8 +43,16 @@
 //   2 producers load the halo but skip the prologue / split / LDS writes
 //   4 consumers idle (barriers only)      5 no weight DMA
 //   8 producers idle (no DMA, no halo)   9 = 8 + no consumer epilogue   10 = 9 + no barriers
+//   11 skip chunks DMA the weights in place of the operand gather
 #ifndef X3_ABLATE
 #define X3_ABLATE 0
+#endif
+// IFD_TRACE=1 builds: shader-cycle stamps (s_memtime) of the first 16 chunk intervals into
+// ConvParams::trace, 64 slots per block: [j] consumer wave 0 at interval start, [16 + j] after
+// its MFMAs are issued; producer wave 4: [48 + j] after the LDS writes of interval j, [32 + j]
+// after its DMA + loads are issued (just before its barrier).
+#ifndef IFD_TRACE
+#define IFD_TRACE 0
 #endif
 
 namespace ifd {
@@ -77,8 +85,10 @@ struct XGeo {
   static constexpr int ITEMS = (2 * NP + NP_T - 1) / NP_T;  // (pixel, channel half) items per producer thread
   static_assert(NP <= XNPMAX && ITEMS == 3, "halo staging: 3 items per producer thread");
 };
-// Every producer interval issues exactly 9 LDS-DMA ops then 10 register loads (barrier arithmetic).
+// Every producer interval issues the chunk's LDS-DMA ops (XDMA3 for a 3x3 chunk, XDMA1 for a skip
+// chunk) then exactly X_LOADS_PER_CHUNK register loads (the barrier's vmcnt arithmetic).
 constexpr int X_LOADS_PER_CHUNK = 2 * 3 + 4;
+constexpr int XDMA3 = 9, XDMA1 = 5;
 
 // Work unit L -> (tile, split z). The S splits of a tile are consecutive L; pixel tiles in groups
 // of 8 get channel-tile IDs 8 apart (conv.hip's XCD-aware map) when the tile count allows. Every
@@ -86,24 +96,36 @@ constexpr int X_LOADS_PER_CHUNK = 2 * 3 + 4;
 // so the decode is shifts and masks on log2 values taken once per kernel.
 struct XDec {
   int lks, lnct, ltx, lty;
-  bool xcd;
+  bool xcd;        // conv.hip's XCD-aware map (pixel tiles in groups of 8)
+  bool blk_major;  // a block's consecutive units = the channel tiles of one pixel tile
 };
 __device__ __forceinline__ XDec x3_dec(const ConvParams& p, int nct) {
   return {__builtin_ctz(p.ksplit), __builtin_ctz(nct), __builtin_ctz(p.tiles_x), __builtin_ctz(p.tiles_y),
-          p.npix_tiles % 8 == 0};
+          p.npix_tiles % 8 == 0, p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0};
 }
-__device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int L, int& z) {
-  z = L & ((1 << d.lks) - 1);
-  const int v = L >> d.lks;
+// Unit u of block b. blk_major (no split-K, pixel tiles a multiple of the grid): block b takes
+// pixel tiles b, b + G, ... and runs all channel tiles of each back to back, so the second
+// channel tile re-reads the same input (3x3 halo and skip operand) from L2 instead of HBM.
+// Otherwise L = b + u G walks the XCD-aware map (S splits of a tile consecutive in L).
+__device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int b, int u, int& z) {
   STile t;
   int bx;
-  if (d.xcd) {
-    const int rr = v & ((8 << d.lnct) - 1);
-    t.ct = rr >> 3;
-    bx = ((v >> (3 + d.lnct)) << 3) + (rr & 7);
+  if (d.blk_major) {
+    z = 0;
+    t.ct = u & ((1 << d.lnct) - 1);
+    bx = b + (int)gridDim.x * (u >> d.lnct);
   } else {
-    t.ct = v & ((1 << d.lnct) - 1);
-    bx = v >> d.lnct;
+    const int L = b + u * (int)gridDim.x;
+    z = L & ((1 << d.lks) - 1);
+    const int v = L >> d.lks;
+    if (d.xcd) {
+      const int rr = v & ((8 << d.lnct) - 1);
+      t.ct = rr >> 3;
+      bx = ((v >> (3 + d.lnct)) << 3) + (rr & 7);
+    } else {
+      t.ct = v & ((1 << d.lnct) - 1);
+      bx = v >> d.lnct;
+    }
   }
   t.x0 = (bx & ((1 << d.ltx) - 1)) * p.TW;
   bx >>= d.ltx;
@@ -122,17 +144,21 @@ template <int XF, bool SKIP, int TW>
 struct XProducer {
   using Geo = XGeo<TW>;
   int ptid, hh;  // hh: channel half (8 of the chunk's 16 channels) this thread stages
+  int lane16;    // 16 * lane: the weight DMA's per-lane byte offset
   int hy[3], hx[3], ldso[3];  // ldso: 16-B slot of the pixel in the hi plane; -1 unused
   int cur_unit = -1;
   rsrc_t r0, r1, ra, rb;
   int off0[3], off1[3];
   int tn0;
-  int skp[4];  // skip segment: image pixel of tile pixel 64 i + lane
+  int skp[4];  // skip segment: image pixel of tile pixel 64 pw + 16 i + lane / 4 (DMA round i)
+  int skq;     // skip segment: byte offset of this lane's swizzled channel quad (see dma)
+  int spf;     // skip segment: image pixel of tile pixel ptid (L2 prefetch, one line per pixel)
   float valid[3];
 
   __device__ __forceinline__ void init(int t) {
     ptid = t;
     hh = t & 1;
+    lane16 = 16 * (t & 63);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int idx = t + i * NP_T, pix = idx >> 1;
@@ -154,9 +180,11 @@ struct XProducer {
     if (SKIP) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = 64 * i + (ptid & 63);
+        const int m = 64 * (ptid >> 6) + 16 * i + ((ptid & 63) >> 2);
         skp[i] = (t.y0 + m / TW) * p.W + t.x0 + m % TW;
       }
+      skq = 16 * ((ptid & 3) ^ ((ptid >> 4) & 3));
+      spf = (t.y0 + ptid / TW) * p.W + t.x0 + ptid % TW;
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -181,21 +209,30 @@ struct XProducer {
     }
   }
 
-  __device__ __forceinline__ void load(XSet& s, const ConvParams& p, int c, int nmain) {
+  __device__ __forceinline__ void load(XSet& s, const ConvParams& p, int c, int nmain, int nskip) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) s.vld[i] = valid[i];
     if (X3_ABLATE == 1 || X3_ABLATE >= 8) return;
     if (SKIP && c >= nmain) {
-      // the skip chunk's operand arrives by LDS-DMA (dma); these only keep the count (one line)
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        s.raw[i][0] = bld4(r0, 0, 0);
-        s.raw[i][1] = bld4(r0, 0, 0);
-      }
-      s.ca[0] = bld4(ra, 0, 0);
-      s.ca[1] = bld4(ra, 0, 0);
-      s.cb[0] = bld4(rb, 0, 0);
-      s.cb[1] = bld4(rb, 0, 0);
+      // The skip chunk's operand arrives by LDS-DMA (dma), issued only two short intervals before
+      // use; one load per thread (= tile pixel: its 128-B line) pulls the operand of skip chunk
+      // c + 4 into L2 so that DMA hits L2. The other loads keep the count fixed (one line).
+      const int cp = min(c + 4, nmain + nskip - 1) - nmain;
+      const int cs = 16 * cp;
+      const bool first = cs < p.sc0;
+      const int sc = first ? p.sc0 : p.sc1;
+      const rsrc_t rs = mkrsrc((first ? p.s0 : p.s1) + (size_t)tn0 * p.H * p.W * sc);
+      // (distinct offsets: identical loads get merged and their copies then wait for vmcnt(0))
+      s.raw[0][0] = bld4(rs, spf * sc * 4, (first ? cs : cs - p.sc0) * 4);
+      s.raw[0][1] = bld4(r0, 0, 16);
+      s.raw[1][0] = bld4(r0, 0, 32);
+      s.raw[1][1] = bld4(r0, 0, 48);
+      s.raw[2][0] = bld4(r0, 0, 64);
+      s.raw[2][1] = bld4(r0, 0, 80);
+      s.ca[0] = bld4(ra, 0, 96);
+      s.ca[1] = bld4(ra, 0, 112);
+      s.cb[0] = bld4(rb, 0, 128);
+      s.cb[1] = bld4(rb, 0, 144);
       return;
     }
     const int cb0 = 16 * c;
@@ -218,12 +255,13 @@ struct XProducer {
     s.cb[1] = bld4(rb, 32 * hh + 16, cb0 * 4);
   }
 
-  // LDS-DMA of chunk c of channel tile ct into ring slot `Wslot`, always XWDMA ops per thread:
+  // LDS-DMA of chunk c of channel tile ct into ring slot `Wslot` (XDMA3 / XDMA1 ops per thread):
   //   3x3 chunk: the weight slab (9 rounds of 1 KiB per producer wave);
   //   skip chunk kk: weights [1][part][h][64][8] (4 KiB, one round) at slot offset 0; the raw fp32
-  //     operand (16 channels of the tile's 256 pixels, from s0 or s1) as 4 quad planes
-  //     [h][q][256 px][4 fp32] at XSKA (wave pw copies plane pw in 4 rounds; the consumer splits
-  //     it in registers); then 4 filler rounds into the slot's tail.
+  //     operand (16 channels = 64 B of each of the tile's 256 pixels, from s0 or s1) pixel-major at
+  //     XSKA, 16 pixels per round (4 lanes per pixel: 16 cache lines per wave-instruction), the
+  //     lane's 16-B quad slot XOR-swizzled by (pixel >> 2) & 3 so the consumers' ds_read_b128 are
+  //     conflict-free.
   __device__ __forceinline__ void dma(const ConvParams& p, int ct, int c, int nmain, int nskip, lds_f* Wslot) const {
     if (X3_ABLATE == 5 || X3_ABLATE >= 8) return;
     const int pw = __builtin_amdgcn_readfirstlane(ptid >> 6);
@@ -232,25 +270,28 @@ struct XProducer {
       const rsrc_t r = mkrsrc(p.wskip + ((size_t)ct * nskip + kk) * (XW / 9));
       const int qb = pw * 64;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(Wslot + 4 * qb), 16,
-                                               16 * (qb + (ptid & 63)), 0, 0, 0);
+                                               lane16, 16 * qb, 0, 0);
       const int cs = 16 * kk;
       const bool first = cs < p.sc0;
       const int sc = first ? p.sc0 : p.sc1;
       const rsrc_t rs = mkrsrc((first ? p.s0 : p.s1) + (size_t)tn0 * p.H * p.W * sc);
-      const int soff = ((first ? cs : cs - p.sc0) + 8 * (pw >> 1) + 4 * (pw & 1)) * 4;
+      const int soff = (first ? cs : cs - p.sc0) * 4;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 4; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(Wslot + XSKA + 4096 * (i >> 2) + pw * 1024 + 256 * (i & 3)),
-            16, skp[i & 3] * sc * 4, soff, 0, 0);
+            X3_ABLATE == 11 ? r : rs, (__attribute__((address_space(3))) void*)(Wslot + XSKA + 16 * (64 * pw + 16 * i)),
+            16, X3_ABLATE == 11 ? 16 * (ptid & 63) : skp[i] * sc * 4 + skq, X3_ABLATE == 11 ? 0 : soff, 0, 0);
       return;
     }
+    // per-lane offset = the loop-invariant 16 * lane (lane16), the round in the scalar offset: a
+    // per-round VALU temporary would share VGPRs with in-flight halo loads and make the compiler
+    // wait for them (vmcnt) before the DMA issues
     const rsrc_t r = mkrsrc(p.wpack + ((size_t)ct * nmain + c) * XW);
 #pragma unroll
     for (int i = 0; i < XWDMA; ++i) {
       const int qb = (i * 4 + pw) * 64;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(Wslot + 4 * qb), 16,
-                                               16 * (qb + (ptid & 63)), 0, 0, 0);
+                                               lane16, 16 * qb, 0, 0);
     }
   }
 
@@ -339,9 +380,9 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
   }
 }
 
-// One 1x1 skip chunk: the raw fp32 operand (quad planes [h][q][256 px][4] at As) is split in
-// registers with the producers' arithmetic (a_hi = f16(a), a_lo = f16(a - a_hi)), then the 3
-// split products x 2 x 2 fragment blocks. pb = tile pixel.
+// One 1x1 skip chunk: the raw fp32 operand (pixel-major [256 px][4 swizzled quads][4] at As) is
+// split in registers with the producers' arithmetic (a_hi = f16(a), a_lo = f16(a - a_hi)), then
+// the 3 split products x 2 x 2 fragment blocks. pb = tile pixel.
 __device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws,
                                              const int (&pb)[2]) {
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
@@ -349,8 +390,9 @@ __device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* A
   f16x8 ah[2], al[2], bs[2], bl[2];
 #pragma unroll
   for (int mr = 0; mr < 2; ++mr) {
-    const f32x4 q0 = *(const lds_f4*)(As + 4 * ((2 * h) * 256 + pb[mr]));
-    const f32x4 q1 = *(const lds_f4*)(As + 4 * ((2 * h + 1) * 256 + pb[mr]));
+    const int sw = (pb[mr] >> 2) & 3;  // quad Q of pixel m sits in slot Q ^ ((m >> 2) & 3)
+    const f32x4 q0 = *(const lds_f4*)(As + 16 * pb[mr] + 4 * ((2 * h) ^ sw));
+    const f32x4 q1 = *(const lds_f4*)(As + 16 * pb[mr] + 4 * ((2 * h + 1) ^ sw));
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float v = j < 4 ? q0[j] : q1[j - 4];
@@ -399,7 +441,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   const int nchu = (nmain + nskip) / S;  // chunks per unit (host: divisible)
   const int J = nu * nchu;
   const XDec dec = x3_dec(p, nct);
-  auto unit_of = [&](int u, int& z) { return x3_unit(p, dec, (int)blockIdx.x + u * G, z); };
+  auto unit_of = [&](int u, int& z) { return x3_unit(p, dec, (int)blockIdx.x, u, z); };
 
   if (consumer) {
     const int h = lane >> 5, l32 = lane & 31;
@@ -539,6 +581,8 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     int kk = 0, u = 0, z = 0;
     STile t = unit_of(0, z);
     for (int j = 0; j < J; ++j) {
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
+        p.trace[64 * blockIdx.x + j] = __builtin_amdgcn_s_memtime();
       const lds_f* Ws = W0 + (j % 3) * XW;
       const int c = z * nchu + kk;  // chunk index within the tile's K stream
       if (kk == nchu - 1 && S == 1 && X3_ABLATE < 9) prefetch(t);
@@ -548,6 +592,8 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       } else {
         consume_skip(acc, Ws + XSKA, Ws, pbs);
       }
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
+        p.trace[64 * blockIdx.x + 16 + j] = __builtin_amdgcn_s_memtime();
       if (++kk == nchu) {
         kk = 0;
         if (X3_ABLATE < 9)
@@ -579,7 +625,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     mainq[jl & 1] = !SKIP || c < nmain;
     P.enter(p, tl, ul);
     P.dma(p, tl.ct, c, nmain, nskip, W0 + (jl % 3) * XW);
-    P.load(s, p, c, nmain);
+    P.load(s, p, c, nmain, nskip);
     if (jl + 1 < J) {
       ++jl;
       if (++kl == nchu) {
@@ -594,21 +640,34 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   issue(s1);  // chunk 1
   P.store(s0, p.act, A0);  // chunk 0 is a 3x3 chunk; waits for its loads, hence its DMA
   XBARRIER_PRODUCER(10);
-  static_assert(X_LOADS_PER_CHUNK == 10 && XWDMA == 9, "barrier vmcnt literals");
+  static_assert(X_LOADS_PER_CHUNK == 10 && XWDMA == XDMA3 && XDMA1 == 5, "barrier vmcnt literals");
   if (X3_ABLATE == 10) return;
-  // interval j: DMA of chunk j+2 (9 ops), halo loads of chunk j+2 (10), LDS writes of chunk j+1,
-  // then the barrier once chunk j+1's DMA (issued in interval j-1) has landed: younger than it
-  // are chunk j+1's 10 loads, chunk j+2's 9 DMA ops and its 10 loads -> vmcnt(29)
+  // interval j: LDS writes of chunk j+1 (its loads were issued one interval ago), then the DMA and
+  // halo loads of chunk j+2, then the barrier once chunk j+1's DMA (issued in interval j-1) has
+  // landed: younger than it are chunk j+1's 10 loads, chunk j+2's DMA ops (9, or 5 for a skip
+  // chunk) and its 10 loads. Writes BEFORE issue: hipcc's vmcnt model does not count LDS-DMA ops,
+  // so a wait for chunk j+1's registers placed after chunk j+2's DMA would also wait for that DMA.
+  auto barrier = [&](int jn) {
+    if (!SKIP || mainq[jn & 1])
+      XBARRIER_PRODUCER(29);
+    else
+      XBARRIER_PRODUCER(25);
+  };
+  auto stamp = [&](int slot, int j) {
+    if (IFD_TRACE && p.trace && ptid == 0 && j < 16) p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
+  };
   for (int j = 0; j < J; j += 2) {
-    const bool m1 = mainq[(j + 1) & 1];
+    if (j + 1 < J && mainq[(j + 1) & 1]) P.store(s1, p.act, A0 + XA);
+    stamp(48, j);
     issue(s0);  // chunk j+2
-    if (j + 1 < J && m1) P.store(s1, p.act, A0 + XA);
-    XBARRIER_PRODUCER(29);
+    stamp(32, j);
+    barrier(j + 2);
     if (j + 1 >= J) break;
-    const bool m2 = mainq[(j + 2) & 1];
+    if (j + 2 < J && mainq[(j + 2) & 1]) P.store(s0, p.act, A0);
+    stamp(48, j + 1);
     issue(s1);  // chunk j+3
-    if (j + 2 < J && m2) P.store(s0, p.act, A0);
-    XBARRIER_PRODUCER(29);
+    stamp(32, j + 1);
+    barrier(j + 3);
   }
 }
 

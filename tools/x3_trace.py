@@ -1,0 +1,36 @@
+"""Development: per-interval cycle stamps of one 3xf16 conv launch (IFD_TRACE build).
+usage: IFD_LIB_PATH=tools/abl/libifd_trace.so python tools/x3_trace.py '<layer match>' [B]"""
+import os, sys
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "face-inpainting-diffusion-models_amd")]
+import numpy as np
+import torch
+from ifd.manifest import make_state_dict
+from ifd.model import DiffusionInpaintingModel
+from ifd.topology import FULL
+match = sys.argv[1]
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "x3trace.bin")
+dev = torch.device("cuda:0")
+m = DiffusionInpaintingModel(FULL, device=dev, precision="3xf16")
+m.load_state_dict(make_state_dict(FULL, seed=1))
+x = torch.randn(B, 3, 256, 256, device=dev); mk = (torch.rand(B, 1, 256, 256, device=dev) > 0.5).float()
+t = torch.full((B,), 500, device=dev)
+with torch.no_grad():
+    m(x, t, masked_image=x, mask=mk)
+    torch.cuda.synchronize()
+    os.environ["IFD_TRACE_MATCH"] = match
+    os.environ["IFD_TRACE_FILE"] = out
+    m(x, t, masked_image=x, mask=mk)
+    torch.cuda.synchronize()
+tr = np.fromfile(out, dtype=np.uint64).reshape(-1, 64).astype(np.int64)
+print(open(out + ".json").read().strip())
+blk = tr[:256]
+cs, ce, pi, ps = blk[:, 0:16], blk[:, 16:32], blk[:, 32:48], blk[:, 48:64]
+np.set_printoptions(linewidth=220)
+med = lambda a: np.median(a, axis=0).astype(int)
+print("interval (consumer start j -> j+1):", med(np.diff(cs, axis=1)))
+print("consumer issue (start -> MFMAs issued):", med(ce - cs))
+print("producer: interval start -> DMA+loads issued:", med(pi[:, 1:] - cs[:, 1:]))
+print("producer: loads issued -> LDS writes done:", med(ps - pi))
+print("producer: LDS writes done -> next consumer start:", med(cs[:, 1:] - ps[:, :-1]))
