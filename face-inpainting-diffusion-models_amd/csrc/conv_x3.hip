@@ -85,8 +85,10 @@ struct XGeo {
   static constexpr int ITEMS = (2 * NP + NP_T - 1) / NP_T;  // (pixel, channel half) items per producer thread
   static_assert(NP <= XNPMAX && ITEMS == 3, "halo staging: 3 items per producer thread");
 };
-// Every producer interval issues the chunk's LDS-DMA ops (XDMA3 for a 3x3 chunk, XDMA1 for a skip
-// chunk) then exactly X_LOADS_PER_CHUNK register loads (the barrier's vmcnt arithmetic).
+// vmcnt ops per chunk, in issue order: a 3x3 chunk = XDMA3 weight DMAs then X_LOADS_PER_CHUNK halo /
+// coefficient register loads; a skip chunk = XDMA1 DMAs (weights, operand) and no register load
+// (the barrier's vmcnt arithmetic). (An L2 prefetch of later skip operands - one line request per
+// tile pixel - measured slower at distances 4 to 8: it holds miss slots the gathers need.)
 constexpr int X_LOADS_PER_CHUNK = 2 * 3 + 4;
 constexpr int XDMA3 = 9, XDMA1 = 5;
 
@@ -150,9 +152,13 @@ struct XProducer {
   rsrc_t r0, r1, ra, rb;
   int off0[3], off1[3];
   int tn0;
-  int skp[4];  // skip segment: image pixel of tile pixel 64 pw + 16 i + lane / 4 (DMA round i)
-  int skq;     // skip segment: byte offset of this lane's swizzled channel quad (see dma)
-  int spf;     // skip segment: image pixel of tile pixel ptid (L2 prefetch, one line per pixel)
+  // Skip segment (per unit). Skip chunks issue DMA only - no register load, no per-chunk VALU: a
+  // dead placeholder load frees its VGPRs for VALU temporaries, the compiler then waits (vmcnt) for
+  // that load before the temporary is written, and as its vmcnt model omits LDS-DMA ops, that wait
+  // also covers the previous chunk's operand DMA: one chunk in flight instead of two.
+  int skp[4];  // image pixel of tile pixel 64 pw + 16 i + lane / 4 (DMA round i): the index of a
+               // strided buffer view (stride = the source's channel count x 4 B)
+  int skq;     // byte offset of this lane's swizzled channel quad (see dma)
   float valid[3];
 
   __device__ __forceinline__ void init(int t) {
@@ -184,7 +190,6 @@ struct XProducer {
         skp[i] = (t.y0 + m / TW) * p.W + t.x0 + m % TW;
       }
       skq = 16 * ((ptid & 3) ^ ((ptid >> 4) & 3));
-      spf = (t.y0 + ptid / TW) * p.W + t.x0 + ptid % TW;
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -199,8 +204,7 @@ struct XProducer {
     }
   }
 
-  // Global loads of chunk c (16 channels; c >= nmain: the 1x1 skip segment) of the entered unit
-  // into set s: exactly X_LOADS_PER_CHUNK loads on every path (see conv_stream.hip SProducer::load).
+  // Global loads of 3x3 chunk c of the entered unit into set s: X_LOADS_PER_CHUNK loads.
   // per-unit state (descriptors, pixel offsets): before the unit's first DMA or load
   __device__ __forceinline__ void enter(const ConvParams& p, const STile& t, int u) {
     if (u != cur_unit) {
@@ -213,28 +217,7 @@ struct XProducer {
 #pragma unroll
     for (int i = 0; i < 3; ++i) s.vld[i] = valid[i];
     if (X3_ABLATE == 1 || X3_ABLATE >= 8) return;
-    if (SKIP && c >= nmain) {
-      // The skip chunk's operand arrives by LDS-DMA (dma), issued only two short intervals before
-      // use; one load per thread (= tile pixel: its 128-B line) pulls the operand of skip chunk
-      // c + 4 into L2 so that DMA hits L2. The other loads keep the count fixed (one line).
-      const int cp = min(c + 4, nmain + nskip - 1) - nmain;
-      const int cs = 16 * cp;
-      const bool first = cs < p.sc0;
-      const int sc = first ? p.sc0 : p.sc1;
-      const rsrc_t rs = mkrsrc((first ? p.s0 : p.s1) + (size_t)tn0 * p.H * p.W * sc);
-      // (distinct offsets: identical loads get merged and their copies then wait for vmcnt(0))
-      s.raw[0][0] = bld4(rs, spf * sc * 4, (first ? cs : cs - p.sc0) * 4);
-      s.raw[0][1] = bld4(r0, 0, 16);
-      s.raw[1][0] = bld4(r0, 0, 32);
-      s.raw[1][1] = bld4(r0, 0, 48);
-      s.raw[2][0] = bld4(r0, 0, 64);
-      s.raw[2][1] = bld4(r0, 0, 80);
-      s.ca[0] = bld4(ra, 0, 96);
-      s.ca[1] = bld4(ra, 0, 112);
-      s.cb[0] = bld4(rb, 0, 128);
-      s.cb[1] = bld4(rb, 0, 144);
-      return;
-    }
+    if (SKIP && c >= nmain) return;  // operand by DMA (see dma)
     const int cb0 = 16 * c;
     if (cb0 < p.c0) {
 #pragma unroll
@@ -274,13 +257,16 @@ struct XProducer {
       const int cs = 16 * kk;
       const bool first = cs < p.sc0;
       const int sc = first ? p.sc0 : p.sc1;
-      const rsrc_t rs = mkrsrc((first ? p.s0 : p.s1) + (size_t)tn0 * p.H * p.W * sc);
+      // strided view of the source image: record = pixel (sc x 4 B), index skp[i], offset skq
+      const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>((first ? p.s0 : p.s1) + (size_t)tn0 * p.H * p.W * sc), (short)(sc * 4), 0x7ffffff0,
+          0x00020000);
       const int soff = (first ? cs : cs - p.sc0) * 4;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            X3_ABLATE == 11 ? r : rs, (__attribute__((address_space(3))) void*)(Wslot + XSKA + 16 * (64 * pw + 16 * i)),
-            16, X3_ABLATE == 11 ? 16 * (ptid & 63) : skp[i] * sc * 4 + skq, X3_ABLATE == 11 ? 0 : soff, 0, 0);
+        __builtin_amdgcn_struct_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(Wslot + XSKA + 16 * (64 * pw + 16 * i)), 16, skp[i], skq,
+            soff, 0, 0);
       return;
     }
     // per-lane offset = the loop-invariant 16 * lane (lane16), the round in the scalar offset: a
@@ -616,13 +602,16 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   XSet s0, s1;
   // Lookahead cursor over the chunk stream: position jl = (unit ul, chunk kl of the unit), the
   // unit's tile decoded once per unit; past the end it stays on the last chunk (re-issued loads /
-  // DMA of identical bytes keep the op counts fixed). mainq[q & 1]: chunk q is a 3x3 chunk.
+  // DMA of identical bytes keep the op counts fixed).
+  // lastmain: the last issued chunk is a 3x3 chunk (an int kept in an SGPR: a bool array here was
+  // materialised through a VGPR that aliased an in-flight load, i.e. a vmcnt wait every interval).
   int jl = 0, ul = 0, kl = 0, zl = 0;
   STile tl = unit_of(0, zl);
-  bool mainq[2] = {true, true};
+  int lastmain = 1, prevmain = 1;  // the last / the previous issued chunk is a 3x3 chunk
   auto issue = [&](XSet& s) {  // DMA + register loads of the cursor's chunk, then advance
-    const int c = zl * nchu + kl;
-    mainq[jl & 1] = !SKIP || c < nmain;
+    const int c = __builtin_amdgcn_readfirstlane(zl * nchu + kl);
+    prevmain = lastmain;
+    lastmain = (!SKIP || c < nmain) ? 1 : 0;
     P.enter(p, tl, ul);
     P.dma(p, tl.ct, c, nmain, nskip, W0 + (jl % 3) * XW);
     P.load(s, p, c, nmain, nskip);
@@ -636,38 +625,44 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       jl += 3;  // parity / ring slot of the clamped repeats: keep writing slot (J - 1) % 3
     }
   };
-  issue(s0);  // chunk 0
-  issue(s1);  // chunk 1
-  P.store(s0, p.act, A0);  // chunk 0 is a 3x3 chunk; waits for its loads, hence its DMA
-  XBARRIER_PRODUCER(10);
+  // Barrier once chunk q's DMA has landed, chunk q+1 being the last issued: younger are chunk q's
+  // register loads (10, none for a skip chunk), then all of chunk q+1 (9 + 10, or 5).
   static_assert(X_LOADS_PER_CHUNK == 10 && XWDMA == XDMA3 && XDMA1 == 5, "barrier vmcnt literals");
+  auto barrier = [&]() {
+    if (!SKIP || (prevmain && lastmain))
+      XBARRIER_PRODUCER(29);
+    else if (prevmain)
+      XBARRIER_PRODUCER(15);
+    else if (lastmain)
+      XBARRIER_PRODUCER(19);
+    else
+      XBARRIER_PRODUCER(5);
+  };
+  issue(s0);  // chunk 0
+  const int main0 = lastmain;
+  issue(s1);  // chunk 1
+  if (main0) P.store(s0, p.act, A0);  // (a split-K unit may start in the skip segment)
+  barrier();
   if (X3_ABLATE == 10) return;
   // interval j: LDS writes of chunk j+1 (its loads were issued one interval ago), then the DMA and
   // halo loads of chunk j+2, then the barrier once chunk j+1's DMA (issued in interval j-1) has
-  // landed: younger than it are chunk j+1's 10 loads, chunk j+2's DMA ops (9, or 5 for a skip
-  // chunk) and its 10 loads. Writes BEFORE issue: hipcc's vmcnt model does not count LDS-DMA ops,
-  // so a wait for chunk j+1's registers placed after chunk j+2's DMA would also wait for that DMA.
-  auto barrier = [&](int jn) {
-    if (!SKIP || mainq[jn & 1])
-      XBARRIER_PRODUCER(29);
-    else
-      XBARRIER_PRODUCER(25);
-  };
+  // landed. Writes BEFORE issue: hipcc's vmcnt model does not count LDS-DMA ops, so a wait for
+  // chunk j+1's registers placed after chunk j+2's DMA would also wait for that DMA.
   auto stamp = [&](int slot, int j) {
     if (IFD_TRACE && p.trace && ptid == 0 && j < 16) p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
   };
   for (int j = 0; j < J; j += 2) {
-    if (j + 1 < J && mainq[(j + 1) & 1]) P.store(s1, p.act, A0 + XA);
+    if (j + 1 < J && lastmain) P.store(s1, p.act, A0 + XA);  // last issued = chunk j+1
     stamp(48, j);
     issue(s0);  // chunk j+2
     stamp(32, j);
-    barrier(j + 2);
+    barrier();
     if (j + 1 >= J) break;
-    if (j + 2 < J && mainq[(j + 2) & 1]) P.store(s0, p.act, A0);
+    if (j + 2 < J && lastmain) P.store(s0, p.act, A0);
     stamp(48, j + 1);
     issue(s1);  // chunk j+3
     stamp(32, j + 1);
-    barrier(j + 3);
+    barrier();
   }
 }
 
@@ -708,7 +703,8 @@ static int launch_x3_tw(const ConvParams& p, int xform, hipStream_t stream) {
 }  // namespace
 
 // Eligible: 3x3, BN = 64, 256-pixel tiles of one image (8 x 32 or 16 x 16), NHWC epilogue, cout a
-// multiple of 64, 16-channel chunks on every source (main and skip), K chunks divisible by the
+// multiple of 64, 16-channel chunks on every source (main and skip; skip sources < 4096 channels: the
+// strided view's 14-bit stride), K chunks divisible by the
 // split, no avg-pool prologue (run_conv feeds those layers a pooled activation instead) nor
 // avg-pool residual without split-K (pooled likewise). Any act, identity or nearest-up residual,
 // 1x1 skip segment.
@@ -716,7 +712,7 @@ bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
   const int nch = p.cin_pad / 16 + (p.wskip ? p.cs_pad / 16 : 0);
   return taps == 9 && xform != XF_DOWN && bn == XBN && p.bm == 256 && (p.TW == 32 || p.TW == 16) &&
          p.TH * p.TW == 256 && p.IMGS == 1 && p.epi == EPI_NHWC && p.cout % XBN == 0 && p.cout_pad == p.cout &&
-         p.c0 % 16 == 0 && p.c1 % 16 == 0 && (!p.wskip || (p.sc0 % 16 == 0 && p.sc1 % 16 == 0)) &&
+         p.c0 % 16 == 0 && p.c1 % 16 == 0 && (!p.wskip || (p.sc0 % 16 == 0 && p.sc1 % 16 == 0 && p.sc0 < 4096 && p.sc1 < 4096)) &&
          p.ksplit >= 1 && nch % p.ksplit == 0 && (!p.res || p.res_xform != XF_DOWN || p.ksplit > 1);
 }
 
