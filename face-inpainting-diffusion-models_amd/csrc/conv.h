@@ -95,6 +95,12 @@ int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t str
 bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn);
 int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream);
 
+// fp32 output-head conv (conv_head.hip): 3x3, cout 6 or 3, NCHW / sampler-step epilogues.
+bool conv_head_eligible(const ConvParams& p, int taps, int xform);
+size_t conv_head_pack_floats(int cin);
+void conv_head_pack(const float* w, int cout, int cin, float* dst);
+int launch_conv_head(const ConvParams& p, const float* wh, hipStream_t stream);
+
 // Shared elementwise step math, also used by the standalone step kernels (sampler.hip).
 __device__ __forceinline__ float ddim_step_value(const StepCoeffs& s, float img, float eps, float noise,
                                                 float gt, float mask, float known) {

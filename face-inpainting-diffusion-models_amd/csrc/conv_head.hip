@@ -1,0 +1,188 @@
+// Output head of the UNet (code/unet.py:196-200, `out`: GroupNorm -> SiLU -> conv 3x3 ch -> 6):
+// fp32 VALU direct convolution with the GroupNorm-apply + SiLU prologue and the NCHW / fused
+// sampler-step epilogues of conv.hip.
+//
+// Why not the MFMA conv kernels: cout = 6 (or 3) fills 6/32 of a 32-wide MFMA tile and the fp32
+// MFMA rate equals the fp32 VALU rate on gfx950 (MI355X_MICROARCH.md), so a GEMM tiling wastes
+// ~5x. Here each thread owns two vertically adjacent output pixels and keeps their 2 x 6
+// accumulators in registers; the weights are wave-uniform, so they arrive by scalar loads and
+// every MAC is one v_fma_f32 with an SGPR operand, each weight serving both pixels. Per 16-channel
+// chunk a block stages the activated 18 x 34 halo of its 16 x 32 tile in LDS (4 quad planes
+// [pixel][4 ch]: a wave's ds_read_b128 of 64 consecutive pixels is conflict-free); a thread reads
+// each halo column of 4 rows once for its 3 x 2 (tap row, pixel) uses. The next chunk's halo
+// loads are in flight in registers during the FMAs.
+//
+// Bound: VALU. Per output pixel 9 * cin * cout FMAs (13.8 kFLOP for cin 128, cout 6) against
+// ~0.6 KB of HBM traffic (4 * cin B of input + the step epilogue's 64 B): 23 FLOP/B, above the
+// 157 TF/s : 8 TB/s balance point of ~20 FLOP/B.
+#include <hip/hip_runtime.h>
+
+#include "conv.h"
+#include "conv_dev.h"
+
+namespace ifd {
+namespace {
+
+constexpr int HD_TW = 32, HD_TH = 16;                          // output tile (one image)
+constexpr int HD_HW = HD_TW + 2, HD_NP = HD_HW * (HD_TH + 2);  // 34 x 18 = 612 halo pixels
+constexpr int HD_NT = 256;                                     // one thread per 2 output pixels
+constexpr int HD_ITEMS = (HD_NP * 4 + HD_NT - 1) / HD_NT;      // (pixel, quad) items per thread: 10
+
+// wh: [cin/16][9 taps][16 ci][8] fp32 (co 0..cout-1, zero padded), bias = p.bias
+template <int CO>
+__global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const float* __restrict__ wh) {
+  __shared__ __attribute__((aligned(16))) float hal[4][HD_NP][4];  // quad plane q: [pixel][4 channels]
+  const int tid = threadIdx.x;
+  const int tiles_x = p.W / HD_TW, tiles_y = p.H / HD_TH;
+  int b = blockIdx.x;
+  const int tx = b % tiles_x;
+  b /= tiles_x;
+  const int ty = b % tiles_y;
+  const int n = b / tiles_y;
+  const int x0 = tx * HD_TW, y0 = ty * HD_TH;
+  const int cin = p.c0;
+  const int nchunk = cin / 16;
+  const float* __restrict__ src = p.in0 + (size_t)n * p.H * p.W * cin;
+
+  // staging items: item i = (halo pixel i >> 2, channel quad i & 3); quad = tid & 3 for every item
+  const int q = tid & 3;
+  int goff[HD_ITEMS];
+  bool inb[HD_ITEMS];
+#pragma unroll
+  for (int k = 0; k < HD_ITEMS; ++k) {
+    const int i = tid + k * HD_NT;
+    const int pix = i >> 2;
+    const int hy = pix / HD_HW, hx = pix - hy * HD_HW;
+    const int y = y0 + hy - 1, x = x0 + hx - 1;
+    inb[k] = i < 4 * HD_NP && y >= 0 && y < p.H && x >= 0 && x < p.W;
+    goff[k] = inb[k] ? (y * p.W + x) * cin + 4 * q : 0;
+  }
+  f32x4 raw[HD_ITEMS];
+  auto load = [&](int ch) {
+#pragma unroll
+    for (int k = 0; k < HD_ITEMS; ++k)
+      raw[k] = inb[k] ? gld4(src + goff[k] + 16 * ch) : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto stage = [&](int ch) {
+    f32x4 ca = {1.f, 1.f, 1.f, 1.f}, cb = {0.f, 0.f, 0.f, 0.f};
+    if (p.act != ACT_NONE) {
+      ca = gld4(p.actA + (size_t)n * cin + 16 * ch + 4 * q);
+      cb = gld4(p.actB + (size_t)n * cin + 16 * ch + 4 * q);
+    }
+#pragma unroll
+    for (int k = 0; k < HD_ITEMS; ++k) {
+      const int i = tid + k * HD_NT;
+      if (i < 4 * HD_NP) {
+        f32x4 v;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float t = raw[k][c];
+          if (p.act != ACT_NONE) {
+            t = ca[c] * t + cb[c];
+            if (p.act == ACT_AFFINE_SILU) t = silu_fast(t);
+          }
+          v[c] = inb[k] ? t : 0.f;  // zero padding of the activated input
+        }
+        *(f32x4*)&hal[q][i >> 2][0] = v;
+      }
+    }
+  };
+
+  const int py = 2 * (tid / HD_TW), px = tid % HD_TW;  // pixels (py, px) and (py + 1, px)
+  const int hp = py * HD_HW + px;                      // halo pixel of tap (0, 0) of the first
+  float acc[2][CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) acc[0][c] = acc[1][c] = 0.f;
+
+  load(0);
+  for (int ch = 0; ch < nchunk; ++ch) {
+    __syncthreads();  // the previous chunk's reads are done
+    stage(ch);
+    __syncthreads();
+    if (ch + 1 < nchunk) load(ch + 1);  // in flight during this chunk's FMAs
+    const float* __restrict__ w = wh + (size_t)ch * 9 * 16 * 8;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        f32x4 v[4];  // halo rows py .. py + 3 of column px + dx
+#pragma unroll
+        for (int hr = 0; hr < 4; ++hr) v[hr] = *(const f32x4*)&hal[qq][hp + hr * HD_HW + dx][0];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy) {
+            const float* wr = w + ((dy * 3 + dx) * 16 + 4 * qq + c) * 8;
+#pragma unroll
+            for (int co = 0; co < CO; ++co) {
+              acc[0][co] = __builtin_fmaf(v[dy][c], wr[co], acc[0][co]);
+              acc[1][co] = __builtin_fmaf(v[dy + 1][c], wr[co], acc[1][co]);
+            }
+          }
+      }
+    }
+  }
+
+  // epilogue (conv.hip's NCHW / DDIM / DDPM paths)
+  const int HWp = p.H * p.W;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+  const size_t pix = (size_t)(y0 + py + r) * p.W + (x0 + px);
+  if (p.epi == EPI_NCHW) {
+#pragma unroll
+    for (int co = 0; co < CO; ++co) p.out[((size_t)n * CO + co) * HWp + pix] = acc[r][co] + p.bias[co];
+    continue;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const size_t o3 = ((size_t)n * 3 + c) * HWp + pix;
+    const size_t om = (size_t)n * HWp + pix;
+    const float eps = acc[r][c] + p.bias[c];
+    const float x = p.img[o3];
+    const float mk = p.sc.inject ? p.mask[om] : 0.f;
+    const float g = p.sc.inject ? p.gt[o3] : 0.f;
+    const float kn = p.sc.inject ? p.known[o3] : 0.f;
+    float v;
+    if (p.epi == EPI_DDIM) {
+      const float nz = p.sc.use_noise ? p.noise[o3] : 0.f;
+      v = ddim_step_value(p.sc, x, eps, nz, g, mk, kn);
+    } else {
+      const float var_v = acc[r][CO > 3 ? c + 3 : c] + p.bias[c + 3];
+      v = ddpm_step_value(p.sc, x, eps, var_v, p.noise[o3], g, mk, kn);
+    }
+    p.img[o3] = v;
+  }
+  }
+}
+
+}  // namespace
+
+bool conv_head_eligible(const ConvParams& p, int taps, int xform) {
+  const bool step = p.epi == EPI_DDIM || p.epi == EPI_DDPM;
+  return taps == 9 && xform == XF_NONE && !p.in1 && p.c1 == 0 && p.c0 % 16 == 0 && p.c0 >= 16 && !p.wskip &&
+         !p.res && (p.epi == EPI_NCHW || step) && (p.cout == 6 || (p.cout == 3 && p.epi != EPI_DDPM)) &&
+         p.H % HD_TH == 0 && p.W % HD_TW == 0 && p.Hin == p.H && p.Win == p.W;
+}
+
+size_t conv_head_pack_floats(int cin) { return (size_t)(cin / 16) * 9 * 16 * 8; }
+
+// w: torch layout [cout][cin][3][3] -> [cin/16][tap][16][8]
+void conv_head_pack(const float* w, int cout, int cin, float* dst) {
+  for (int ch = 0; ch < cin / 16; ++ch)
+    for (int tap = 0; tap < 9; ++tap)
+      for (int c = 0; c < 16; ++c)
+        for (int co = 0; co < 8; ++co)
+          dst[((size_t)(ch * 9 + tap) * 16 + c) * 8 + co] =
+              co < cout ? w[((size_t)co * cin + ch * 16 + c) * 9 + tap] : 0.f;
+}
+
+int launch_conv_head(const ConvParams& p, const float* wh, hipStream_t stream) {
+  const int blocks = p.N * (p.H / HD_TH) * (p.W / HD_TW);
+  if (p.cout == 6)
+    hipLaunchKernelGGL(conv_head_kernel<6>, dim3(blocks), dim3(HD_NT), 0, stream, p, wh);
+  else
+    hipLaunchKernelGGL(conv_head_kernel<3>, dim3(blocks), dim3(HD_NT), 0, stream, p, wh);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ifd

@@ -15,7 +15,7 @@ int launch_gn_finalize2(const float* part0, int E0, float cnt0, int C0, const fl
 void launch_pack_input(const float* x, const float* a, const float* m, int mode, int N, int HW, float* out,
                        hipStream_t s);
 void launch_temb(const int64_t* t, const float* freqs, int mc, const float* w0t, const float* b0, const float* w2t,
-                 const float* b2, int E, int N, float* emb, hipStream_t s);
+                 const float* b2, int E, int N, float* h1, float* emb, hipStream_t s);
 void launch_emb_proj(const float* emb, int E, int N, const float* wt, const float* b, int J, float* out,
                      hipStream_t s);
 void launch_attention(const float* qkv, int N, int T, int C, float scale, float* out, hipStream_t s);

@@ -46,75 +46,95 @@ void launch_pack_input(const float* x, const float* a, const float* m, int mode,
 }
 
 // ---------------------------------------------------------------------------------------------
-// timestep_embedding (code/nn.py:51-61) + time_embed MLP (code/unet.py:44-48).
-// One block per image; weights pre-transposed to [in][out] so each thread's loads coalesce.
-__global__ __launch_bounds__(512) void temb_kernel(const int64_t* __restrict__ t, const float* __restrict__ freqs,
-                                                   int mc, const float* __restrict__ w0t, const float* __restrict__ b0,
-                                                   const float* __restrict__ w2t, const float* __restrict__ b2,
-                                                   int E, float* __restrict__ emb) {
-  extern __shared__ float sm[];
-  float* te = sm;        // [mc]
-  float* h1 = sm + mc;   // [E]
-  const int n = blockIdx.x, tid = threadIdx.x;
-  const float tf = (float)t[n];
-  const int half = mc / 2;
-  for (int i = tid; i < half; i += blockDim.x) {
-    const float arg = tf * freqs[i];
-    te[i] = cosf(arg);
-    te[half + i] = sinf(arg);
-  }
-  __syncthreads();
-  for (int j = tid; j < E; j += blockDim.x) {
-    float acc = 0.f;
-    for (int k = 0; k < mc; ++k) acc += w0t[(size_t)k * E + j] * te[k];
-    h1[j] = silu_f(acc + b0[j]);
-  }
-  __syncthreads();
-  for (int j = tid; j < E; j += blockDim.x) {
-    float acc = 0.f;
-    for (int k = 0; k < E; ++k) acc += w2t[(size_t)k * E + j] * h1[k];
-    emb[(size_t)n * E + j] = acc + b2[j];
-  }
-}
-
-void launch_temb(const int64_t* t, const float* freqs, int mc, const float* w0t, const float* b0, const float* w2t,
-                 const float* b2, int E, int N, float* emb, hipStream_t s) {
-  hipLaunchKernelGGL(temb_kernel, dim3(N), dim3(512), (mc + E) * sizeof(float), s, t, freqs, mc, w0t, b0, w2t, b2, E,
-                     emb);
-}
-
-// All 30 ResBlock emb projections of one eval in one launch (code/nn.py:167-170,199):
-//   Eall[n][j] = sum_k Wt[k][j] * silu(emb[n][k]) + b[j],   j over the concatenated [2*Cout] rows.
-constexpr int EP_NB = 16;
-__global__ __launch_bounds__(256) void emb_proj_kernel(const float* __restrict__ emb, int E, int N,
-                                                       const float* __restrict__ wt, const float* __restrict__ b,
-                                                       int J, float* __restrict__ out) {
-  extern __shared__ float se[];  // [EP_NB][E]
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  for (int nb = 0; nb < N; nb += EP_NB) {
-    const int nn = min(EP_NB, N - nb);
+// The embedding MLPs as skinny GEMMs: out[n][j] = post(sum_k pre(in)[n][k] * Wt[k][j] + b[j]) for
+// the N <= 16 images of a pass, Wt pre-transposed to [K][J] so a wave's weight loads coalesce.
+//   time_embed.0 (code/unet.py:44-48, nn.py:51-61): pre = timestep_embedding(t), post = SiLU
+//   time_embed.2: pre = identity (the stored h1 is already SiLU'd), post = identity
+//   all 30 ResBlock emb_layers (nn.py:167-170,199) in one launch: pre = SiLU, post = identity
+// Block = 64 columns x 4 K-quarters (one wave each); the input rows sit in LDS as [k][16] so a
+// k step is 1 coalesced weight load + 4 broadcast ds_read_b128 + 16 FMAs; the quarters are summed
+// in a fixed order (deterministic). Bound: the weight stream (K x J x 4 B, read once per pass).
+enum SkPre : int { SK_PRE_NONE = 0, SK_PRE_SILU = 1, SK_PRE_TEMB = 2 };
+constexpr int SK_NB = 16;  // images per pass
+constexpr int SK_JB = 64;  // columns per block
+__global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ in, const int64_t* __restrict__ t,
+                                                     const float* __restrict__ freqs, int pre, int post_silu, int K,
+                                                     int N, const float* __restrict__ wt,
+                                                     const float* __restrict__ b, int J, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float sk[];  // [K][SK_NB] inputs, then [4][SK_NB][SK_JB]
+  float* red = sk + (size_t)K * SK_NB;
+  const int tid = threadIdx.x, jj = tid & (SK_JB - 1), kq = tid / SK_JB;
+  const int j = blockIdx.x * SK_JB + jj;
+  const int kc = K / 4, k0 = kq * kc;
+  for (int nb = 0; nb < N; nb += SK_NB) {
+    const int nn = min(SK_NB, N - nb);
     __syncthreads();
-    for (int i = threadIdx.x; i < nn * E; i += blockDim.x) se[i] = silu_f(emb[(size_t)nb * E + i]);
-    __syncthreads();
-    if (j < J) {
-      float acc[EP_NB];
-#pragma unroll
-      for (int q = 0; q < EP_NB; ++q) acc[q] = 0.f;
-      for (int k = 0; k < E; ++k) {
-        const float w = wt[(size_t)k * J + j];
-#pragma unroll
-        for (int q = 0; q < EP_NB; ++q) acc[q] += w * se[q * E + k];
+    for (int i = tid; i < K * SK_NB; i += 256) {
+      const int kk = i / SK_NB, q = i % SK_NB;
+      float v = 0.f;
+      if (q < nn) {
+        if (pre == SK_PRE_TEMB) {
+          const int half = K / 2;
+          const float arg = (float)t[nb + q] * freqs[kk < half ? kk : kk - half];
+          v = kk < half ? cosf(arg) : sinf(arg);
+        } else {
+          v = in[(size_t)(nb + q) * K + kk];
+          if (pre == SK_PRE_SILU) v = silu_f(v);
+        }
       }
-      const float bj = b[j];
-      for (int q = 0; q < nn; ++q) out[(size_t)(nb + q) * J + j] = acc[q] + bj;
+      sk[i] = v;
+    }
+    __syncthreads();
+    float acc[SK_NB];
+#pragma unroll
+    for (int q = 0; q < SK_NB; ++q) acc[q] = 0.f;
+    if (j < J) {
+#pragma unroll 4
+      for (int kk = k0; kk < k0 + kc; ++kk) {
+        const float w = wt[(size_t)kk * J + j];
+        const f32x4* s4 = reinterpret_cast<const f32x4*>(sk + (size_t)kk * SK_NB);
+#pragma unroll
+        for (int g = 0; g < SK_NB / 4; ++g) {
+          const f32x4 s = s4[g];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[4 * g + c] += w * s[c];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < SK_NB; ++q) red[(kq * SK_NB + q) * SK_JB + jj] = acc[q];
+    __syncthreads();
+    for (int i = tid; i < SK_NB * SK_JB; i += 256) {
+      const int q = i / SK_JB, c = i % SK_JB, jo = blockIdx.x * SK_JB + c;
+      if (q < nn && jo < J) {
+        float v = ((red[(0 * SK_NB + q) * SK_JB + c] + red[(1 * SK_NB + q) * SK_JB + c]) +
+                   red[(2 * SK_NB + q) * SK_JB + c]) + red[(3 * SK_NB + q) * SK_JB + c];
+        v += b[jo];
+        if (post_silu) v = silu_f(v);
+        out[(size_t)(nb + q) * J + jo] = v;
+      }
     }
   }
 }
 
+static void launch_skinny(const float* in, const int64_t* t, const float* freqs, int pre, int post_silu, int K, int N,
+                          const float* wt, const float* b, int J, float* out, hipStream_t s) {
+  const size_t lds = ((size_t)K * SK_NB + 4 * SK_NB * SK_JB) * sizeof(float);
+  hipLaunchKernelGGL(skinny_kernel, dim3((J + SK_JB - 1) / SK_JB), dim3(256), lds, s, in, t, freqs, pre, post_silu, K,
+                     N, wt, b, J, out);
+}
+
+// emb = time_embed(timestep_embedding(t, mc)); h1 (SiLU'd first layer) in `h1` [N][E]
+void launch_temb(const int64_t* t, const float* freqs, int mc, const float* w0t, const float* b0, const float* w2t,
+                 const float* b2, int E, int N, float* h1, float* emb, hipStream_t s) {
+  launch_skinny(nullptr, t, freqs, SK_PRE_TEMB, 1, mc, N, w0t, b0, E, h1, s);
+  launch_skinny(h1, nullptr, nullptr, SK_PRE_NONE, 0, E, N, w2t, b2, E, emb, s);
+}
+
+// All 30 ResBlock emb projections of one eval: Eall[n][j] = sum_k Wt[k][j] * silu(emb[n][k]) + b[j]
 void launch_emb_proj(const float* emb, int E, int N, const float* wt, const float* b, int J, float* out,
                      hipStream_t s) {
-  hipLaunchKernelGGL(emb_proj_kernel, dim3((J + 255) / 256), dim3(256), EP_NB * E * sizeof(float), s, emb, E, N, wt,
-                     b, J, out);
+  launch_skinny(emb, nullptr, nullptr, SK_PRE_SILU, 0, E, N, wt, b, J, out, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -18,6 +18,7 @@ struct ConvW {
   size_t x3_off = 0;   // float offset of the 3xf16 split packing (pack_conv_x3), 0 if none
   size_t x3s_off = 0;  // ... of the 1x1 skip segment
   bool x3_ok = false;  // every weight within the split's range (|w| < 32): the layer may run 3xf16
+  size_t head_off = 0;  // float offset of the output-head packing (conv_head.hip), 0 if none
   std::string wname, bname, swname, sbname;  // source parameter names
 };
 
@@ -137,7 +138,7 @@ class Model {
   int ws_B_ = 0;
   // workspace carve (float offsets), valid for ws_B_
   size_t o_x0_ = 0, o_bufs_[3] = {0, 0, 0}, o_t1_ = 0, o_qkv_ = 0, o_ao_ = 0, o_A_ = 0, o_B_ = 0, o_part_ = 0,
-         o_emb_ = 0, o_E_ = 0, o_split_ = 0, o_pool_ = 0, o_pool2_ = 0;
+         o_emb_ = 0, o_h1_ = 0, o_E_ = 0, o_split_ = 0, o_pool_ = 0, o_pool2_ = 0;
   size_t split_floats_ = 0;
   std::vector<size_t> o_hs_;
   // GroupNorm granule statistics: one area per activation buffer (hs, bufs, t1); stat_ holds the

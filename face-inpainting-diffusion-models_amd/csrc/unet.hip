@@ -364,6 +364,9 @@ int Model::finalize() {
   }
   plan_gn(gn_out_);
   plan_conv(conv_out_);
+  conv_out_.head_off = 0;
+  if (conv_out_.taps == 9 && conv_out_.cin % 16 == 0 && (conv_out_.cout == 6 || conv_out_.cout == 3))
+    conv_out_.head_off = reserve(conv_head_pack_floats(conv_out_.cin));
 
   std::vector<float> blob(n, 0.f);
   auto put = [&](size_t off, const std::vector<float>& v) { std::copy(v.begin(), v.end(), blob.begin() + off); };
@@ -428,6 +431,8 @@ int Model::finalize() {
   }
   fill_gn(gn_out_);
   fill_conv(conv_out_);
+  if (conv_out_.head_off)
+    conv_head_pack(host_[conv_out_.wname].data(), conv_out_.cout, conv_out_.cin, blob.data() + conv_out_.head_off);
 
   if (wblob_) IFD_CHECK_HIP(hipFree(wblob_));
   wblob_ = nullptr;
@@ -520,6 +525,7 @@ int Model::ensure_workspace(int B) {
   o_pool_ = reserve(maxpool);
   o_pool2_ = reserve(maxpool);  // pooled residual (a down-ResBlock keeps cin == cout)
   o_emb_ = reserve((size_t)B * emb_dim_);
+  o_h1_ = reserve((size_t)B * emb_dim_);
   o_E_ = reserve((size_t)B * emb_total_);
   // granule statistics areas: a tensor at resolution r with C channels has at most
   // max(r^2/64, 1) entries of C/4 (mean, M2) pairs per image
@@ -620,7 +626,9 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   } else if (x3_geo) {  // not split-eligible after all: the fp32 kernels' own geometry
     conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8);
   }
-  const bool use_stream = use_x3 || (stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn));
+  // the output head (cout 6): fp32 VALU kernel in every precision mode
+  const bool use_head = !use_x3 && cw.head_off && conv_head_eligible(p, cw.taps, xf);
+  const bool use_stream = !use_head && (use_x3 || (stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn)));
   // fused GroupNorm statistics of the output (single-image tiles, no split-K; not mode 1)
   p.gstat = nullptr;
   p.gstat_E = 0;
@@ -656,7 +664,9 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
 #endif
   hipEvent_t e0;
   prof_begin(s, &e0);
+  if (use_head) p.ksplit = 1;
   int e = use_x3       ? launch_conv_x3(p, xf, s)
+          : use_head   ? launch_conv_head(p, wblob_ + cw.head_off, s)
           : use_stream ? launch_conv_stream(p, xf, stream_mode, s)
                        : launch_conv(p, cw.taps, xf, cw.bn, s);
   if (p.gstat)
@@ -694,10 +704,12 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     char nm[160];
     if (prof_layers_)
       snprintf(nm, sizeof(nm), "%s<%d,%d,%d,%d> r%d %d+%d->%d skip%d",
-               use_x3 ? "conv_x3" : (use_stream ? "conv_stream" : "conv_kernel"), p.bm,
+               use_x3 ? "conv_x3" : (use_head ? "conv_head" : (use_stream ? "conv_stream" : "conv_kernel")), p.bm,
                cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
     else if (use_x3)
       snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d>", xf, cw.has_skip ? "true" : "false", p.TW);
+    else if (use_head)
+      snprintf(nm, sizeof(nm), "conv_head_kernel<%d>", cw.cout);
     else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
       snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
     else if (use_stream)
@@ -815,7 +827,7 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   prof_begin(s, &p0);
   launch_pack_input(x, a, m, pack_mode, B, R * R, x0, s);
   launch_temb(t, wblob_ + freqs_, mc, wblob_ + te_w0_, wblob_ + te_b0_, wblob_ + te_w2_, wblob_ + te_b2_, emb_dim_, B,
-              ws_ + o_emb_, s);
+              ws_ + o_h1_, ws_ + o_emb_, s);
   launch_emb_proj(ws_ + o_emb_, emb_dim_, B, wblob_ + embw_, wblob_ + embb_, emb_total_, ws_ + o_E_, s);
   prof_end(s, p0, "input_pack+temb+emb_proj", 2.0 * B * (double)emb_dim_ * (mc + emb_dim_ + emb_total_),
            4.0 * B * (double)R * R * (7 + 16) + 4.0 * emb_dim_ * (double)emb_total_);
