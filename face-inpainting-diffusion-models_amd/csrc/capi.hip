@@ -100,6 +100,11 @@ int ifd_profile_enable(ifd_handle* h, int on) {
   return h->model->profile_enable(on);
 }
 
+int ifd_profile_filter(ifd_handle* h, const char* prefix) {
+  if (!h) { set_error("null handle"); return 2; }
+  return h->model->profile_filter(prefix);
+}
+
 int ifd_profile_report(ifd_handle* h, char* buf, int64_t buflen) {
   if (!h || !buf || buflen <= 0) { set_error("ifd_profile_report: bad argument"); return 2; }
   std::string js;

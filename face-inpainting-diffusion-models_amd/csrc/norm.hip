@@ -195,7 +195,7 @@ int launch_gn(const float* p0, int c0, const float* p1, int c1, int N, int HW, c
 // pixels, the same for all granules). The convs that PRODUCE a tensor write them from their
 // epilogue (conv.hip / conv_stream.hip, ConvParams::gstat), so the GroupNorm of the next layer
 // needs no pass over the tensor; tensors without them get gn_granules_kernel (one streaming pass).
-// gn_finalize2 merges the entries of each granule and the granules of each group — across the
+// gn_finalize2 combines the entries of each granule and the granules of each group — across the
 // two concat sources when the GroupNorm input is cat(h, skip) — in float64, in a fixed order.
 
 struct GnGranuleParams {
@@ -271,71 +271,66 @@ struct GnFinalize2Params {
   float* A; float* B;  // [N][C]
 };
 
-__device__ __forceinline__ void merge64(double& n, double& m, double& m2, double nb, double mb, double m2b) {
-  const double tot = n + nb;
-  if (nb <= 0) return;
-  const double d = mb - m;
-  m += d * (nb / tot);
-  m2 += m2b + d * d * (n * nb / tot);
-  n = tot;
+// Block-wide fp64 sum in a fixed order (wave xor-tree, then the 4 wave sums in order): deterministic.
+__device__ __forceinline__ double block_sum64(double v, double* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // sh reuse across calls
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double s = sh[0];
+  for (int i = 1; i < GN_NT / 64; ++i) s += sh[i];
+  return s;
 }
 
-// one block per (group g, image n): for each granule of the group the 256 threads merge strided
-// entries in float64, a fixed-shape LDS tree merges the threads, and the granules are merged in
-// channel order; then the group's channels get A/B
+// one block per (group g, image n). Every entry of a source holds `cnt` values (mean, M2), so the
+// group statistics are two fp64 passes over the group's entries (all granules, both concat
+// sources): mean = sum(cnt * mean_e) / sum(cnt), then M2 = sum(M2_e + cnt * (mean_e - mean)^2) —
+// the exact combination of equal-count partials, with sums instead of per-entry Chan merges (no
+// division per entry). Then the group's channels get A/B.
 __global__ __launch_bounds__(GN_NT) void gn_finalize2_kernel(GnFinalize2Params p) {
-  __shared__ double rn[GN_NT], rm[GN_NT], r2[GN_NT];
-  __shared__ float sres[2];
+  __shared__ double sh[GN_NT / 64];
   const int g = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
   const int C = p.s0.C + p.s1.C;
   const int Cg = C / GN_G;
-  double gn = 0.0, gm = 0.0, gm2 = 0.0;
-  for (int c = g * Cg; c < (g + 1) * Cg; c += 4) {
-    const bool first = c < p.s0.C;
-    const GnSrc& S = first ? p.s0 : p.s1;
-    const int gr = (first ? c : c - p.s0.C) >> 2;
-    const int QP = S.C >> 2;
-    double cn = 0.0, cm = 0.0, cm2 = 0.0;
-    for (int e = tid; e < S.E; e += GN_NT) {
-      const float* o = S.part + (((size_t)n * S.E + e) * QP + gr) * 2;
-      merge64(cn, cm, cm2, (double)S.cnt, (double)o[0], (double)o[1]);
+  const int ng = Cg / 4;  // granules of the group
+  // granule k of the group -> (source, granule index); entries strided over the block
+  auto walk = [&](auto&& f) {
+    for (int k = 0; k < ng; ++k) {
+      const int c = g * Cg + 4 * k;
+      const bool first = c < p.s0.C;
+      const GnSrc& S = first ? p.s0 : p.s1;
+      const int gr = (first ? c : c - p.s0.C) >> 2;
+      const int QP = S.C >> 2;
+      const float* base = S.part + ((size_t)n * S.E * QP + gr) * 2;
+      for (int e = tid; e < S.E; e += GN_NT) f(base + (size_t)e * QP * 2, (double)S.cnt);
     }
-    rn[tid] = cn;
-    rm[tid] = cm;
-    r2[tid] = cm2;
-    __syncthreads();
-    for (int w = GN_NT / 2; w > 0; w >>= 1) {
-      if (tid < w) {
-        double an = rn[tid], am = rm[tid], a2 = r2[tid];
-        merge64(an, am, a2, rn[tid + w], rm[tid + w], r2[tid + w]);
-        rn[tid] = an;
-        rm[tid] = am;
-        r2[tid] = a2;
-      }
-      __syncthreads();
-    }
-    if (gn == 0.0) {
-      gn = rn[0]; gm = rm[0]; gm2 = r2[0];
-    } else {
-      merge64(gn, gm, gm2, rn[0], rm[0], r2[0]);
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    sres[0] = (float)gm;
-    sres[1] = (float)(1.0 / sqrt(gm2 / gn + (double)p.eps));
-  }
-  __syncthreads();
-  const float mean = sres[0], rstd = sres[1];
+  };
+  double sn = 0.0, sm = 0.0;
+  walk([&](const float* o, double cnt) {
+    sn += cnt;
+    sm += cnt * (double)o[0];
+  });
+  const double ntot = block_sum64(sn, sh);
+  const double mean = block_sum64(sm, sh) / ntot;
+  double s2 = 0.0;
+  walk([&](const float* o, double cnt) {
+    const double d = (double)o[0] - mean;
+    s2 += (double)o[1] + cnt * d * d;
+  });
+  const double m2 = block_sum64(s2, sh);
+  const float meanf = (float)mean;
+  const float rstd = (float)(1.0 / sqrt(m2 / ntot + (double)p.eps));
   for (int c = g * Cg + tid; c < (g + 1) * Cg; c += GN_NT) {
     const float a = rstd * p.gamma[c];
-    const float b = p.beta[c] - mean * a;
+    const float b = p.beta[c] - meanf * a;
     float A = a, B = b;
     if (p.emb) {
       const float sc = 1.0f + p.emb[(size_t)n * p.emb_stride + p.emb_off + c];
-      const float sh = p.emb[(size_t)n * p.emb_stride + p.emb_off + C + c];
+      const float sh2 = p.emb[(size_t)n * p.emb_stride + p.emb_off + C + c];
       A = a * sc;
-      B = b * sc + sh;
+      B = b * sc + sh2;
     }
     p.A[(size_t)n * C + c] = A;
     p.B[(size_t)n * C + c] = B;

@@ -70,6 +70,7 @@ class Model {
   int64_t weight_bytes() const { return (int64_t)wblob_floats_ * 4; }
   // Event-based per-launch profiler (records on the launch stream; read after a sync).
   int profile_enable(int on);
+  int profile_filter(const char* prefix);  // record only launches whose name starts with prefix ("" = all)
   int profile_report(std::string& json);
   int64_t workspace_bytes() const { return (int64_t)ws_floats_ * 4; }
   // Conv arithmetic: IFD_PREC_FP32 (exact fp32 MFMA) or IFD_PREC_3XF16 (split f16 MFMA, fp32-accurate)
@@ -107,11 +108,12 @@ class Model {
   };
   bool prof_on_ = false;
   bool prof_layers_ = false;  // profile_enable(h, 2): key conv launches by layer shape
+  std::string prof_filter_;
   std::vector<ProfRec> prof_;
   std::vector<hipEvent_t> ev_pool_;
   size_t ev_used_ = 0;
   hipEvent_t take_event();
-  void prof_begin(hipStream_t s, hipEvent_t* e0);
+  void prof_begin(hipStream_t s, hipEvent_t* e0, const char* name);
   void prof_end(hipStream_t s, hipEvent_t e0, const std::string& name, double flops, double bytes);
 
   ifd_config cfg_;

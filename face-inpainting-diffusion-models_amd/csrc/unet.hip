@@ -37,9 +37,12 @@ hipEvent_t Model::take_event() {
   return ev_pool_[ev_used_++];
 }
 
-void Model::prof_begin(hipStream_t s, hipEvent_t* e0) {
+void Model::prof_begin(hipStream_t s, hipEvent_t* e0, const char* name) {
   *e0 = nullptr;
   if (!prof_on_) return;
+  // name filter (profile_filter): record only the launches whose name starts with it, so a timed
+  // region pays the event packets for the kernel it measures and not for every launch
+  if (!prof_filter_.empty() && (!name || strncmp(name, prof_filter_.c_str(), prof_filter_.size()) != 0)) return;
   *e0 = take_event();
   if (*e0) (void)hipEventRecord(*e0, s);
 }
@@ -50,6 +53,11 @@ void Model::prof_end(hipStream_t s, hipEvent_t e0, const std::string& name, doub
   if (!e1) return;
   (void)hipEventRecord(e1, s);
   prof_.push_back({name, flops, bytes, e0, e1});
+}
+
+int Model::profile_filter(const char* prefix) {
+  prof_filter_ = prefix ? prefix : "";
+  return 0;
 }
 
 int Model::profile_enable(int on) {
@@ -603,7 +611,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     }
     if ((pool_in || pool_res) && conv_x3_eligible(q, cw.taps, pool_in ? (int)XF_NONE : xf, cw.bn)) {
       hipEvent_t pe;
-      prof_begin(s, &pe);
+      prof_begin(s, &pe, "act_pool");
       int e = 0;
       if (pool_in) e = launch_act_pool(in0, c0, N, Hin, act, A, Bc, ws_ + o_pool_, s);
       if (!e && pool_res) e = launch_act_pool(res, cw.cout, N, resH, ACT_NONE, nullptr, nullptr, ws_ + o_pool2_, s);
@@ -662,8 +670,33 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     p.trace = tbuf;
   }
 #endif
+  char nm[160] = "";
+  double flops = 0.0, bytes = 0.0;
+  if (prof_on_) {
+    // algorithmic work: 2*MAC over real channels; bytes = activations in + weights + out (once each)
+    const int cin_real = (&cw == &conv_in_) ? cfg_.in_channels : cw.cin;
+    const double pix = (double)N * H * H;
+    flops = 2.0 * pix * cw.cout * ((double)cw.taps * cin_real + (cw.has_skip ? cw.cs : 0));
+    bytes = 4.0 * ((double)N * Hin * Hin * (c0 + c1) + pix * cw.cout + (double)cw.cout * cw.cin * cw.taps +
+                   (cw.has_skip ? pix * cw.cs : 0) + (res ? pix * cw.cout : 0));
+    if (prof_layers_)
+      snprintf(nm, sizeof(nm), "%s<%d,%d,%d,%d> r%d %d+%d->%d skip%d",
+               use_x3 ? "conv_x3" : (use_head ? "conv_head" : (use_stream ? "conv_stream" : "conv_kernel")), p.bm,
+               cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
+    else if (use_x3)
+      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d>", xf, cw.has_skip ? "true" : "false", p.TW);
+    else if (use_head)
+      snprintf(nm, sizeof(nm), "conv_head_kernel<%d>", cw.cout);
+    else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
+      snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
+    else if (use_stream)
+      snprintf(nm, sizeof(nm), "conv_stream_kernel<%d,%d>", xf, getenv("IFD_STREAM_CW") ? atoi(getenv("IFD_STREAM_CW")) : 8);
+    else  // (BM,BN,WGM,WGN,TAPS,XF)
+      snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%s,%d,%d>", p.bm, cw.bn,
+               (p.bm == 256 || cw.bn == 32) ? "4,1" : "2,2", cw.taps, xf);
+  }
   hipEvent_t e0;
-  prof_begin(s, &e0);
+  prof_begin(s, &e0, nm);
   if (use_head) p.ksplit = 1;
   int e = use_x3       ? launch_conv_x3(p, xf, s)
           : use_head   ? launch_conv_head(p, wblob_ + cw.head_off, s)
@@ -694,31 +727,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   }
 #endif
   if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, s);
-  if (prof_on_) {
-    // algorithmic work: 2*MAC over real channels; bytes = activations in + weights + out (once each)
-    const int cin_real = (&cw == &conv_in_) ? cfg_.in_channels : cw.cin;
-    const double pix = (double)N * H * H;
-    const double flops = 2.0 * pix * cw.cout * ((double)cw.taps * cin_real + (cw.has_skip ? cw.cs : 0));
-    const double bytes = 4.0 * ((double)N * Hin * Hin * (c0 + c1) + pix * cw.cout + (double)cw.cout * cw.cin * cw.taps +
-                                (cw.has_skip ? pix * cw.cs : 0) + (res ? pix * cw.cout : 0));
-    char nm[160];
-    if (prof_layers_)
-      snprintf(nm, sizeof(nm), "%s<%d,%d,%d,%d> r%d %d+%d->%d skip%d",
-               use_x3 ? "conv_x3" : (use_head ? "conv_head" : (use_stream ? "conv_stream" : "conv_kernel")), p.bm,
-               cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
-    else if (use_x3)
-      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d>", xf, cw.has_skip ? "true" : "false", p.TW);
-    else if (use_head)
-      snprintf(nm, sizeof(nm), "conv_head_kernel<%d>", cw.cout);
-    else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
-      snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
-    else if (use_stream)
-      snprintf(nm, sizeof(nm), "conv_stream_kernel<%d,%d>", xf, getenv("IFD_STREAM_CW") ? atoi(getenv("IFD_STREAM_CW")) : 8);
-    else  // (BM,BN,WGM,WGN,TAPS,XF)
-      snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%s,%d,%d>", p.bm, cw.bn,
-               (p.bm == 256 || cw.bn == 32) ? "4,1" : "2,2", cw.taps, xf);
-    prof_end(s, e0, nm, flops, bytes);
-  }
+  if (prof_on_ && e0) prof_end(s, e0, nm, flops, bytes);
   if (e) {
     set_error(std::string("conv launch failed: ") + hipGetErrorString((hipError_t)e));
     return 1;
@@ -766,7 +775,7 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
   float* t1 = ws_ + o_t1_;
   const int H = r.xf == XF_UP ? 2 * Hin : (r.xf == XF_DOWN ? Hin / 2 : Hin);
   hipEvent_t g0;
-  prof_begin(s, &g0);
+  prof_begin(s, &g0, "groupnorm_stats");
   (void)part;
   int e = run_gn(in0, c0, in1, c1, N, Hin * Hin, r.gn1, nullptr, 0, 0, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, Hin * Hin, c0 + c1));
@@ -774,7 +783,7 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
   if (run_conv(r.conv1, in0, c0, in1, c1, N, Hin, H, r.xf, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
                0, t1, EPI_NHWC, s))
     return 1;
-  prof_begin(s, &g0);
+  prof_begin(s, &g0, "groupnorm_stats");
   e = run_gn(t1, r.cout, nullptr, 0, N, H * H, r.gn2, ws_ + o_E_, emb_total_, r.emb_off, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, H * H, r.cout));
   IFD_REQUIRE(e == 0, "gn launch");
@@ -790,7 +799,7 @@ int Model::run_attn(const AttnP& a, const float* in, int N, int Hin, float* out,
   float* ao = ws_ + o_ao_;
   const int T = Hin * Hin;
   hipEvent_t g0;
-  prof_begin(s, &g0);
+  prof_begin(s, &g0, "groupnorm_stats");
   int e = run_gn(in, a.C, nullptr, 0, N, T, a.gn, nullptr, 0, 0, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, T, a.C));
   IFD_REQUIRE(e == 0, "gn launch");
@@ -799,7 +808,7 @@ int Model::run_attn(const AttnP& a, const float* in, int N, int Hin, float* out,
     return 1;
   const float scale = (float)(1.0 / std::sqrt(std::sqrt((double)cfg_.num_head_channels)));
   IFD_REQUIRE(cfg_.num_head_channels == 64, "attention kernel is specialised for 64-channel heads");
-  prof_begin(s, &g0);
+  prof_begin(s, &g0, "attention_kernel");
   launch_attention(qkv, N, T, a.C, scale, ao, s);
   prof_end(s, g0, "attention_kernel", 4.0 * N * (double)T * T * a.C, 4.0 * N * (double)T * a.C * 4);
   return run_conv(a.proj, ao, a.C, nullptr, 0, N, Hin, Hin, XF_NONE, ACT_NONE, nullptr, nullptr, nullptr, 0, nullptr,
@@ -824,7 +833,7 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
     gn_fused_ = !(gf && gf[0] == '0');
   }
   hipEvent_t p0;
-  prof_begin(s, &p0);
+  prof_begin(s, &p0, "input_pack+temb+emb_proj");
   launch_pack_input(x, a, m, pack_mode, B, R * R, x0, s);
   launch_temb(t, wblob_ + freqs_, mc, wblob_ + te_w0_, wblob_ + te_b0_, wblob_ + te_w2_, wblob_ + te_b2_, emb_dim_, B,
               ws_ + o_h1_, ws_ + o_emb_, s);
@@ -899,7 +908,7 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   // out: GN -> SiLU -> conv 3x3 -> [B,6,H,W] (or the fused sampler update)
   float* A = ws_ + o_A_;
   float* Bc = ws_ + o_B_;
-  prof_begin(s, &p0);
+  prof_begin(s, &p0, "groupnorm_stats");
   int e = run_gn(cur, cur_c, nullptr, 0, B, R * R, gn_out_, nullptr, 0, 0, A, Bc, s);
   prof_end(s, p0, "groupnorm_stats", 0.0, gn_bytes(B, R * R, cur_c));
   IFD_REQUIRE(e == 0, "gn launch");

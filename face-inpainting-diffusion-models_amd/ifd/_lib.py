@@ -47,6 +47,7 @@ EXPORTS = {
     "ifd_version": (ctypes.c_char_p, []),
     "ifd_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ifd_profile_report": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]),
+    "ifd_profile_filter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     "ifd_num_params": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "ifd_param_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), c_i64p,
                                       ctypes.POINTER(ctypes.c_int)]),

@@ -105,6 +105,9 @@ int ifd_blend(const float* result, const float* gt, const float* mask, int64_t B
  * its stream; after the caller synchronises, ifd_profile_report writes a JSON summary per kernel
  * name {"count", "ms", "flops" (algorithmic 2*MAC), "bytes" (algorithmic)} and clears it. */
 int ifd_profile_enable(ifd_handle* h, int on);  /* 0 off, 1 by kernel, 2 by kernel + layer shape */
+/* Record only the launches whose kernel name starts with `prefix` ("" or NULL: all), so a timed
+ * region carries event packets only around the kernel it measures. */
+int ifd_profile_filter(ifd_handle* h, const char* prefix);
 int ifd_profile_report(ifd_handle* h, char* buf, int64_t buflen);
 const char* ifd_version(void);
 
