@@ -221,7 +221,120 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
     for (int q = 0; q < 8; ++q) out[((size_t)n * T + tq) * C + head * AT_CH + u + 8 * q] = acc[q];
 }
 
+// The same attention on fp32 MFMA (v_mfma_f32_32x32x2_f32: an exact fp32 fma chain at the fp32
+// vector rate, 1/16 of the f16 matrix rate - attention is 0.1 % of the FLOPs, so exactness wins),
+// for T a multiple of 32 up to 256. Block = (n, head, 128 queries), 4 waves x 32 queries; the
+// head's K (pre-scaled) and V for all T keys sit in LDS. Per wave:
+//   S^T = K Q^T as KT = T/32 tiles of 32 keys x 32 queries: lane (query l32, half h) gets the
+//     keys 8(r>>2) + 4h + (r&3) of each tile in its 16 accumulator registers; the channel order
+//     of the 32 k-steps is permuted (half h supplies channel 32h + t) on both operands.
+//   softmax over keys: in-register max / exp / sum plus one exchange with lane ^ 32 (the other
+//     key half), then multiply by the reciprocal - the arithmetic of attention_kernel.
+//   O = P V: P is used straight from the accumulators as the A operand (lane (query, h) supplies
+//     key 8(r>>2) + 4h + (r&3) of k-step (tile, r)), V from LDS as B; lane l32 = channel on output.
+constexpr int AM_KS = 68;  // K row stride (floats): ds_read_b128 of 32 rows conflict-free
+constexpr int AM_VS = 72;  // V row stride: rows 4 keys apart (the two lane halves) 32 banks apart
+template <int KT>
+__global__ __launch_bounds__(256, 1) void attention_mfma_kernel(const float* __restrict__ qkv, int C, float scale,
+                                                                float* __restrict__ out) {
+  constexpr int T = 32 * KT;
+  extern __shared__ __attribute__((aligned(16))) float am[];
+  float* Ks = am;                 // [T][AM_KS]
+  float* Vs = am + T * AM_KS;     // [T][AM_VS]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int head = blockIdx.y, n = blockIdx.z;
+  const size_t rs = 3 * (size_t)C;
+  const float* base = qkv + (size_t)n * T * rs + head * AT_CH;
+  for (int i = tid; i < T * (AT_CH / 4); i += 256) {
+    const int row = i / (AT_CH / 4), c4 = 4 * (i % (AT_CH / 4));
+    f32x4 kv = gld4(base + (size_t)row * rs + C + c4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kv[j] = kv[j] * scale;
+    *(f32x4*)(Ks + row * AM_KS + c4) = kv;
+    *(f32x4*)(Vs + row * AM_VS + c4) = gld4(base + (size_t)row * rs + 2 * C + c4);
+  }
+  __syncthreads();
+  const int q0 = blockIdx.x * 128 + 32 * w;
+  if (q0 >= T) return;
+  float qv[32];  // Q[q0 + l32][32h .. 32h + 32) * scale
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const f32x4 v = gld4(base + (size_t)(q0 + l32) * rs + 32 * h + 4 * j);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) qv[4 * j + c] = v[c] * scale;
+  }
+  f32x16 s[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kt][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 kf = *(const f32x4*)(Ks + (kt * 32 + l32) * AM_KS + 32 * h + 4 * j);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[c], qv[4 * j + c], s[kt], 0, 0, 0);
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = expf(s[kt][r] - mx);
+      s[kt][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.0f / sum;
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o0[r] = o1[r] = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pw = s[kt][r] * inv;
+      const float* vr = Vs + (kt * 32 + 8 * (r >> 2) + 4 * h + (r & 3)) * AM_VS + l32;
+      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(pw, vr[0], o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(pw, vr[32], o1, 0, 0, 0);
+    }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int q = q0 + 8 * (r >> 2) + 4 * h + (r & 3);
+    float* o = out + ((size_t)n * T + q) * C + head * AT_CH + l32;
+    o[0] = o0[r];
+    o[32] = o1[r];
+  }
+}
+
+template <int KT>
+static void launch_attention_mfma(const float* qkv, int N, int C, float scale, float* out, hipStream_t s) {
+  constexpr int T = 32 * KT;
+  const size_t lds = (size_t)T * (AM_KS + AM_VS) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_mfma_kernel<KT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  dim3 grid((T + 127) / 128, C / AT_CH, N);
+  hipLaunchKernelGGL(attention_mfma_kernel<KT>, grid, dim3(256), lds, s, qkv, C, scale, out);
+}
+
 void launch_attention(const float* qkv, int N, int T, int C, float scale, float* out, hipStream_t s) {
+  if (C % AT_CH == 0) {
+    if (T == 256) return launch_attention_mfma<8>(qkv, N, C, scale, out, s);
+    if (T == 128) return launch_attention_mfma<4>(qkv, N, C, scale, out, s);
+    if (T == 64) return launch_attention_mfma<2>(qkv, N, C, scale, out, s);
+    if (T == 32) return launch_attention_mfma<1>(qkv, N, C, scale, out, s);
+  }
   dim3 grid((T + AT_QB - 1) / AT_QB, C / AT_CH, N);
   hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, T, C, scale, out);
 }
