@@ -88,6 +88,9 @@ int conv_pick_bn(int cout, int taps, int H, int W, int N);
 // Tile geometry + split-K choice shared by the launcher and the workspace planner.
 void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool x3 = false);
 int launch_splitk_reduce(const ConvParams& p, hipStream_t stream);
+// splitk_reduce + the GroupNorm granule statistics of the output into p.gstat (E entries per image
+// of cnt values each); p.gstat must hold N * E * cout/4 * 2 floats with E = max(H*W / 64, 1).
+int launch_splitk_gstat(const ConvParams& p, int* E, float* cnt, hipStream_t stream);
 // Persistent streaming kernel for the wide layers (conv_stream.hip).
 bool conv_stream_eligible(const ConvParams& p, int taps, int xform, int bn);
 int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t stream);

@@ -624,6 +624,99 @@ __global__ void splitk_reduce_kernel(ConvParams p) {
   p.out[i] = v;
 }
 
+// Split-K reduction that also writes the GroupNorm granule statistics of its output (a split
+// kernel's units end in raw slabs, so it has no per-tile statistics epilogue). Block = (slice of
+// SKG_SL pixels x 64 channel quads, image n); thread = (quad, pixel lane of 4). Per pixel: the slabs
+// summed in slab order, + bias, + residual - splitk_reduce_kernel's arithmetic - stored, and folded
+// into shifted sums (K = the lane's first value); the quad's 4 channels and the 4 pixel lanes merge
+// in a fixed order (Chan) into granule entry (n, slice) of the quad: the entry layout of the conv
+// epilogues (gstat[n][e][cout/4] = (mean, M2), e = slice, cnt = 4 * SKG_SL values).
+constexpr int SKG_SL = 64;
+__global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
+  __shared__ float red[4][64][3];
+  const int q = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int QP = p.cout / 4;
+  const int nqb = (QP + 63) / 64;
+  const int e = blockIdx.x / nqb, qq = (blockIdx.x % nqb) * 64 + q;
+  const int n = blockIdx.y;
+  const int HW = p.H * p.W;
+  const int slice = HW < SKG_SL ? HW : SKG_SL;
+  const bool act = qq < QP;
+  const size_t tot = (size_t)p.N * HW * p.cout;
+  f32x4 K = {0.f, 0.f, 0.f, 0.f}, s1 = K, s2 = K;
+  float cnt = 0.f;
+  if (act) {
+    const f32x4 b = gld4(p.bias + 4 * qq);
+    for (int i = pl; i < slice; i += 4) {
+      const int px = e * slice + i;
+      const size_t idx = ((size_t)n * HW + px) * p.cout + 4 * qq;
+      f32x4 acc = gld4(p.part + idx);
+      for (int z = 1; z < p.ksplit; ++z) acc += gld4(p.part + (size_t)z * tot + idx);
+      f32x4 v = acc + b;
+      if (p.res) {
+        const int x = px % p.W, y = px / p.W;
+        f32x4 rv;
+        if (p.res_xform == XF_NONE) {
+          rv = gld4(p.res + idx);
+        } else if (p.res_xform == XF_UP) {
+          rv = gld4(p.res + ((size_t)(n * p.res_H + (y >> 1)) * p.res_W + (x >> 1)) * p.cout + 4 * qq);
+        } else {
+          const size_t b0 = ((size_t)(n * p.res_H + 2 * y) * p.res_W + 2 * x) * p.cout + 4 * qq;
+          const size_t rs = (size_t)p.res_W * p.cout;
+          const f32x4 r00 = gld4(p.res + b0), r01 = gld4(p.res + b0 + p.cout);
+          const f32x4 r10 = gld4(p.res + b0 + rs), r11 = gld4(p.res + b0 + rs + p.cout);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float s = r00[j];
+            s = s + r01[j];
+            s = s + r10[j];
+            s = s + r11[j];
+            rv[j] = s / 4.0f;
+          }
+        }
+        v = rv + v;
+      }
+      gst4(p.out + idx, v);
+      if (cnt == 0.f) K = v;
+      const f32x4 d = v - K;
+      s1 += d;
+      s2 += d * d;
+      cnt += 1.f;
+    }
+  }
+  GStat g = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    GStat st;
+    st.n = cnt;
+    st.mean = cnt > 0.f ? K[j] + s1[j] / cnt : 0.f;
+    st.m2 = cnt > 0.f ? fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f) : 0.f;
+    g = j == 0 ? st : gmerge(g, st);
+  }
+  red[pl][q][0] = g.n;
+  red[pl][q][1] = g.mean;
+  red[pl][q][2] = g.m2;
+  __syncthreads();
+  if (pl == 0 && act) {
+    GStat a = {red[0][q][0], red[0][q][1], red[0][q][2]};
+    for (int l = 1; l < 4; ++l) a = gmerge(a, GStat{red[l][q][0], red[l][q][1], red[l][q][2]});
+    float* o = p.gstat + (((size_t)n * (HW / slice) + e) * QP + qq) * 2;
+    o[0] = a.mean;
+    o[1] = a.m2;
+  }
+}
+
+int launch_splitk_gstat(const ConvParams& p, int* E, float* cnt, hipStream_t stream) {
+  const int HW = p.H * p.W;
+  const int slice = HW < SKG_SL ? HW : SKG_SL;
+  if (HW % slice != 0 || p.cout % 4 != 0 || !p.gstat) return (int)hipErrorInvalidValue;
+  *E = HW / slice;
+  *cnt = 4.0f * slice;
+  const int nqb = (p.cout / 4 + 63) / 64;
+  hipLaunchKernelGGL(splitk_gstat_kernel, dim3(*E * nqb, p.N), dim3(256), 0, stream, p);
+  return (int)hipGetLastError();
+}
+
 int launch_splitk_reduce(const ConvParams& p, hipStream_t stream) {
   const size_t tot = (size_t)p.N * p.H * p.W * p.cout;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, p);

@@ -726,7 +726,19 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     }
   }
 #endif
-  if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, s);
+  if (!e && p.ksplit > 1) {
+    // the reduction writes the output's GroupNorm granule statistics when it has a stat area
+    auto it = stat_area_.find(out);
+    if (gn_fused_ && epi == EPI_NHWC && it != stat_area_.end() && cw.cout % 4 == 0) {
+      p.gstat = it->second;
+      int E = 0;
+      float cnt = 0.f;
+      e = launch_splitk_gstat(p, &E, &cnt, s);
+      if (!e) stat_[out] = StatRec{p.gstat, E, cnt, cw.cout};
+    } else {
+      e = launch_splitk_reduce(p, s);
+    }
+  }
   if (prof_on_ && e0) prof_end(s, e0, nm, flops, bytes);
   if (e) {
     set_error(std::string("conv launch failed: ") + hipGetErrorString((hipError_t)e));
