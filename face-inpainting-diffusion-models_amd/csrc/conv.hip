@@ -568,6 +568,7 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
     // 3xf16 split kernel (conv_x3.hip): 256-pixel tiles of one image (8 x 32 or 16 x 16) whatever
     // the tile count (persistent grid); nchunks = 16-channel chunks of the whole K stream
     if (bn == 64 && W >= 16 && H >= 256 / (W < 32 ? W : 32)) bm = 256;
+    if (bn == 64 && W == 8 && H == 8 && N % 4 == 0) bm = 256;  // four whole 8 x 8 images per tile
   } else if (allow256 && bn == 64 && W >= 32 && H >= 8) {
     const long blocks256 = (long)N * (H / 8) * (W / 32) * (p.cout_pad / bn);
     if (blocks256 >= 512) bm = 256;
@@ -586,7 +587,8 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
   int S = 1;
   if (x3 && bm == 256) {
     // persistent units: split K until the units cover the 256 CUs, keeping >= 4 chunks per unit
-    while (S < 8 && blocks * S < 256 && nchunks % (2 * S) == 0 && nchunks / (2 * S) >= 4) S *= 2;
+    const int minch = W == 8 ? 2 : 4;  // the 8x8 layers: few units, split down to 2 chunks
+    while (S < 8 && blocks * S < 256 && nchunks % (2 * S) == 0 && nchunks / (2 * S) >= minch) S *= 2;
   } else {
     // split K until the grid covers ~2 blocks per CU, keeping >= 4 chunks per split
     while (S < 8 && blocks * S < 512 && nchunks / (2 * S) >= 4) S *= 2;
@@ -630,14 +632,16 @@ __global__ void splitk_reduce_kernel(ConvParams p) {
 // summed in slab order, + bias, + residual - splitk_reduce_kernel's arithmetic - stored, and folded
 // into shifted sums (K = the lane's first value); the quad's 4 channels and the 4 pixel lanes merge
 // in a fixed order (Chan) into granule entry (n, slice) of the quad: the entry layout of the conv
-// epilogues (gstat[n][e][cout/4] = (mean, M2), e = slice, cnt = 4 * SKG_SL values).
+// epilogues (gstat[n][e][cout/4] = (mean, M2), e = slice, cnt = 4 * SKG_SL values). 16 quads x
+// 16 pixel lanes per block: enough blocks even for the 8x8 layers (one slice per image).
 constexpr int SKG_SL = 64;
+constexpr int SKG_Q = 16, SKG_PL = 256 / SKG_Q;
 __global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
-  __shared__ float red[4][64][3];
-  const int q = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  __shared__ float red[SKG_PL][SKG_Q][3];
+  const int q = threadIdx.x % SKG_Q, pl = threadIdx.x / SKG_Q;
   const int QP = p.cout / 4;
-  const int nqb = (QP + 63) / 64;
-  const int e = blockIdx.x / nqb, qq = (blockIdx.x % nqb) * 64 + q;
+  const int nqb = (QP + SKG_Q - 1) / SKG_Q;
+  const int e = blockIdx.x / nqb, qq = (blockIdx.x % nqb) * SKG_Q + q;
   const int n = blockIdx.y;
   const int HW = p.H * p.W;
   const int slice = HW < SKG_SL ? HW : SKG_SL;
@@ -647,7 +651,7 @@ __global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
   float cnt = 0.f;
   if (act) {
     const f32x4 b = gld4(p.bias + 4 * qq);
-    for (int i = pl; i < slice; i += 4) {
+    for (int i = pl; i < slice; i += SKG_PL) {
       const int px = e * slice + i;
       const size_t idx = ((size_t)n * HW + px) * p.cout + 4 * qq;
       f32x4 acc = gld4(p.part + idx);
@@ -684,14 +688,16 @@ __global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
       cnt += 1.f;
     }
   }
-  GStat g = {0.f, 0.f, 0.f};
+  GStat g = {0.f, 0.f, 0.f};  // a lane without pixels (slices smaller than the lanes) stays empty
+  if (cnt > 0.f) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    GStat st;
-    st.n = cnt;
-    st.mean = cnt > 0.f ? K[j] + s1[j] / cnt : 0.f;
-    st.m2 = cnt > 0.f ? fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f) : 0.f;
-    g = j == 0 ? st : gmerge(g, st);
+    for (int j = 0; j < 4; ++j) {
+      GStat st;
+      st.n = cnt;
+      st.mean = K[j] + s1[j] / cnt;
+      st.m2 = fmaxf(s2[j] - s1[j] * (s1[j] / cnt), 0.f);
+      g = j == 0 ? st : gmerge(g, st);
+    }
   }
   red[pl][q][0] = g.n;
   red[pl][q][1] = g.mean;
@@ -699,7 +705,8 @@ __global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
   __syncthreads();
   if (pl == 0 && act) {
     GStat a = {red[0][q][0], red[0][q][1], red[0][q][2]};
-    for (int l = 1; l < 4; ++l) a = gmerge(a, GStat{red[l][q][0], red[l][q][1], red[l][q][2]});
+    for (int l = 1; l < SKG_PL; ++l)
+      if (red[l][q][0] > 0.f) a = gmerge(a, GStat{red[l][q][0], red[l][q][1], red[l][q][2]});
     float* o = p.gstat + (((size_t)n * (HW / slice) + e) * QP + qq) * 2;
     o[0] = a.mean;
     o[1] = a.m2;
@@ -712,7 +719,7 @@ int launch_splitk_gstat(const ConvParams& p, int* E, float* cnt, hipStream_t str
   if (HW % slice != 0 || p.cout % 4 != 0 || !p.gstat) return (int)hipErrorInvalidValue;
   *E = HW / slice;
   *cnt = 4.0f * slice;
-  const int nqb = (p.cout / 4 + 63) / 64;
+  const int nqb = (p.cout / 4 + SKG_Q - 1) / SKG_Q;
   hipLaunchKernelGGL(splitk_gstat_kernel, dim3(*E * nqb, p.N), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }

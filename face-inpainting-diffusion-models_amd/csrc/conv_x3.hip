@@ -63,11 +63,11 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) f16x8 lds_h8;
 
 constexpr int XBN = 64;
-constexpr int XNPMAX = 340;                    // halo pixels of the largest tile (8 x 32 -> 10 x 34)
-constexpr int XA = 4 * XNPMAX * 4;             // floats per A stage (4 planes x 340 px x 16 B)
+constexpr int XNPMAX = 400;                    // halo pixels of the largest tile (4 images x 10 x 10)
+constexpr int XA = 4 * XNPMAX * 4;             // floats per A stage (4 planes x 400 px x 16 B)
 constexpr int XW = 9 * 2 * 2 * XBN * 4;        // floats per weight-ring slot (36 KiB)
 constexpr int XWDMA = XW / 4 / NP_T;           // 16-B LDS-DMA rounds per producer thread (9)
-constexpr int X_LDS_FLOATS = 2 * XA + 3 * XW;  // 38528 floats = 150.5 KiB
+constexpr int X_LDS_FLOATS = 2 * XA + 3 * XW;  // 40448 floats = 158 KiB
 constexpr int XSKA = 1024;                     // skip chunk slot: weights [0, XSKA), operand planes after
 constexpr float kLo = 2048.0f;                 // 2^11
 static_assert(XW % (4 * NP_T) == 0, "weight slab must be whole DMA rounds");
@@ -76,20 +76,23 @@ static_assert(XSKA + 2 * 4096 <= XW, "skip chunk slot layout");
 #define XBARRIER_CONSUMER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #define XBARRIER_PRODUCER(N) asm volatile("s_waitcnt vmcnt(" #N ") lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-// Tile of 256 output pixels of one image, TW x TH; halo (TW + 2) x (TH + 2).
+// Tile of 256 output pixels: TW x TH of one image (TW = 32, 16), or TW = 8: four whole 8 x 8
+// images (the 8x8 layers), one per consumer wave; halo (TW + 2) x (TH + 2) per image.
 template <int TW>
 struct XGeo {
-  static constexpr int TH = 256 / TW;
+  static constexpr int IMG = TW == 8 ? 4 : 1;               // images per tile
+  static constexpr int TH = 256 / (TW * IMG);
   static constexpr int HW = TW + 2;
-  static constexpr int NP = HW * (TH + 2);                  // 340 (8 x 32), 324 (16 x 16)
+  static constexpr int HP = HW * (TH + 2);                  // halo pixels per image
+  static constexpr int NP = IMG * HP;                       // 340 (8 x 32), 324 (16 x 16), 400 (4 x 8 x 8)
   static constexpr int ITEMS = (2 * NP + NP_T - 1) / NP_T;  // (pixel, channel half) items per producer thread
-  static_assert(NP <= XNPMAX && ITEMS == 3, "halo staging: 3 items per producer thread");
+  static constexpr int LOADS = 2 * ITEMS + 4;               // register loads per 3x3 chunk (vmcnt arithmetic)
+  static_assert(NP <= XNPMAX && (ITEMS == 3 || (IMG == 4 && ITEMS == 4)), "halo staging items");
 };
-// vmcnt ops per chunk, in issue order: a 3x3 chunk = XDMA3 weight DMAs then X_LOADS_PER_CHUNK halo /
+// vmcnt ops per chunk, in issue order: a 3x3 chunk = XDMA3 weight DMAs then XGeo::LOADS halo /
 // coefficient register loads; a skip chunk = XDMA1 DMAs (weights, operand) and no register load
 // (the barrier's vmcnt arithmetic). (An L2 prefetch of later skip operands - one line request per
 // tile pixel - measured slower at distances 4 to 8: it holds miss slots the gathers need.)
-constexpr int X_LOADS_PER_CHUNK = 2 * 3 + 4;
 constexpr int XDMA3 = 9, XDMA1 = 5;
 
 // Work unit L -> (tile, split z). The S splits of a tile are consecutive L; pixel tiles in groups
@@ -97,13 +100,13 @@ constexpr int XDMA3 = 9, XDMA1 = 5;
 // divisor is a power of two (run_conv requires power-of-two sizes; S, cout / 64 in {1, 2, 4, 8}),
 // so the decode is shifts and masks on log2 values taken once per kernel.
 struct XDec {
-  int lks, lnct, ltx, lty;
+  int lks, lnct, ltx, lty, limg;
   bool xcd;        // conv.hip's XCD-aware map (pixel tiles in groups of 8)
   bool blk_major;  // a block's consecutive units = the channel tiles of one pixel tile
 };
 __device__ __forceinline__ XDec x3_dec(const ConvParams& p, int nct) {
   return {__builtin_ctz(p.ksplit), __builtin_ctz(nct), __builtin_ctz(p.tiles_x), __builtin_ctz(p.tiles_y),
-          p.npix_tiles % 8 == 0, p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0};
+          __builtin_ctz(p.IMGS), p.npix_tiles % 8 == 0, p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0};
 }
 // Unit u of block b. blk_major (no split-K, pixel tiles a multiple of the grid): block b takes
 // pixel tiles b, b + G, ... and runs all channel tiles of each back to back, so the second
@@ -132,25 +135,29 @@ __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int
   t.x0 = (bx & ((1 << d.ltx) - 1)) * p.TW;
   bx >>= d.ltx;
   t.y0 = (bx & ((1 << d.lty) - 1)) * p.TH;
-  t.n0 = bx >> d.lty;
+  t.n0 = (bx >> d.lty) << d.limg;
   return t;
 }
 
+template <int ITEMS>
 struct XSet {
-  f32x4 raw[3][2];
+  f32x4 raw[ITEMS][2];
   f32x4 ca[2], cb[2];
-  float vld[3];
+  float vld[ITEMS];
 };
 
 template <int XF, bool SKIP, int TW>
 struct XProducer {
   using Geo = XGeo<TW>;
+  static constexpr int IT = Geo::ITEMS;
+  using Set = XSet<IT>;
   int ptid, hh;  // hh: channel half (8 of the chunk's 16 channels) this thread stages
   int lane16;    // 16 * lane: the weight DMA's per-lane byte offset
-  int hy[3], hx[3], ldso[3];  // ldso: 16-B slot of the pixel in the hi plane; -1 unused
+  int hi[IT], hy[IT], hx[IT], ldso[IT];  // image of the tile, halo row / column; ldso: 16-B slot of
+                                         // the pixel in the hi plane, -1 unused
   int cur_unit = -1;
   rsrc_t r0, r1, ra, rb;
-  int off0[3], off1[3];
+  int off0[IT], off1[IT];
   int tn0;
   // Skip segment (per unit). Skip chunks issue DMA only - no register load, no per-chunk VALU: a
   // dead placeholder load frees its VGPRs for VALU temporaries, the compiler then waits (vmcnt) for
@@ -159,17 +166,19 @@ struct XProducer {
   int skp[4];  // image pixel of tile pixel 64 pw + 16 i + lane / 4 (DMA round i): the index of a
                // strided buffer view (stride = the source's channel count x 4 B)
   int skq;     // byte offset of this lane's swizzled channel quad (see dma)
-  float valid[3];
+  float valid[IT];
 
   __device__ __forceinline__ void init(int t) {
     ptid = t;
     hh = t & 1;
     lane16 = 16 * (t & 63);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < IT; ++i) {
       const int idx = t + i * NP_T, pix = idx >> 1;
-      hy[i] = pix / Geo::HW;
-      hx[i] = pix - hy[i] * Geo::HW;
+      hi[i] = pix / Geo::HP;
+      const int rem = pix - hi[i] * Geo::HP;
+      hy[i] = rem / Geo::HW;
+      hx[i] = rem - hy[i] * Geo::HW;
       ldso[i] = idx < 2 * Geo::NP ? hh * Geo::NP + pix : -1;
     }
   }
@@ -187,24 +196,25 @@ struct XProducer {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = 64 * (ptid >> 6) + 16 * i + ((ptid & 63) >> 2);
-        skp[i] = (t.y0 + m / TW) * p.W + t.x0 + m % TW;
+        const int mi = m / (Geo::TH * TW), mp = m % (Geo::TH * TW);  // image of the tile, its pixel
+        skp[i] = mi * p.H * p.W + (t.y0 + mp / TW) * p.W + t.x0 + mp % TW;
       }
       skq = 16 * ((ptid & 3) ^ ((ptid >> 4) & 3));
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < IT; ++i) {
       const int y = t.y0 + hy[i] - 1, x = t.x0 + hx[i] - 1;
       const bool inb = ldso[i] >= 0 && y >= 0 && y < p.H && x >= 0 && x < p.W;
       int sy = y, sx = x;
       if (XF == XF_UP) { sy = y >> 1; sx = x >> 1; }
-      const int sp = inb ? sy * p.Win + sx : 0;
+      const int sp = inb ? (hi[i] * p.Hin + sy) * p.Win + sx : 0;
       valid[i] = inb ? 1.f : 0.f;
       off0[i] = (sp * p.c0 + 8 * hh) * 4;
       off1[i] = (sp * p.c1 + 8 * hh) * 4;
     }
   }
 
-  // Global loads of 3x3 chunk c of the entered unit into set s: X_LOADS_PER_CHUNK loads.
+  // Global loads of 3x3 chunk c of the entered unit into set s: Geo::LOADS loads.
   // per-unit state (descriptors, pixel offsets): before the unit's first DMA or load
   __device__ __forceinline__ void enter(const ConvParams& p, const STile& t, int u) {
     if (u != cur_unit) {
@@ -213,21 +223,21 @@ struct XProducer {
     }
   }
 
-  __device__ __forceinline__ void load(XSet& s, const ConvParams& p, int c, int nmain, int nskip) {
+  __device__ __forceinline__ void load(Set& s, const ConvParams& p, int c, int nmain, int nskip) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) s.vld[i] = valid[i];
+    for (int i = 0; i < IT; ++i) s.vld[i] = valid[i];
     if (X3_ABLATE == 1 || X3_ABLATE >= 8) return;
     if (SKIP && c >= nmain) return;  // operand by DMA (see dma)
     const int cb0 = 16 * c;
     if (cb0 < p.c0) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
+      for (int i = 0; i < IT; ++i) {
         s.raw[i][0] = bld4(r0, off0[i], cb0 * 4);
         s.raw[i][1] = bld4(r0, off0[i] + 16, cb0 * 4);
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
+      for (int i = 0; i < IT; ++i) {
         s.raw[i][0] = bld4(r1, off1[i], (cb0 - p.c0) * 4);
         s.raw[i][1] = bld4(r1, off1[i] + 16, (cb0 - p.c0) * 4);
       }
@@ -292,10 +302,10 @@ struct XProducer {
   }
 
   // prologue + split: hi plane at slot ldso, lo plane 2 planes further
-  __device__ __forceinline__ void store(const XSet& s, int act, lds_f* As) const {
+  __device__ __forceinline__ void store(const Set& s, int act, lds_f* As) const {
     if (X3_ABLATE == 1 || X3_ABLATE == 2 || X3_ABLATE >= 8) return;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < IT; ++i) {
       if (ldso[i] >= 0) {
         f16x8 h8, l8;
 #pragma unroll
@@ -437,7 +447,8 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr) {
       const int m = wm0 + mr * 32 + l32;
-      pb[mr] = (m / TW) * Geo::HW + (m % TW);
+      const int mi = m / (Geo::TH * TW), mp = m % (Geo::TH * TW);  // image of the tile, its pixel
+      pb[mr] = mi * Geo::HP + (mp / TW) * Geo::HW + (mp % TW);
       pbs[mr] = m;
     }
     auto zero = [&]() {
@@ -463,8 +474,10 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       return ((lin / TW) * p.W + lin % TW) * p.cout * 4;
     };
     const int mstep = (32 / TW) * p.W * p.cout * 4;
+    // the wave's 64 pixels: rows of one image (8x8 tiles: the whole image wm0 / 64 of the tile)
+    const int wimg = wm0 / (Geo::TH * TW), wrow = (wm0 % (Geo::TH * TW)) / TW;
     auto vbase = [&](const STile& t) {
-      return (((t.y0 + wm0 / TW) * p.W + t.x0 + 4 * h) * p.cout + t.ct * XBN + l32) * 4;
+      return (((wimg * p.H + t.y0 + wrow) * p.W + t.x0 + 4 * h) * p.cout + t.ct * XBN + l32) * 4;
     };
     auto prefetch = [&](const STile& t) {
 #pragma unroll
@@ -554,8 +567,9 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           g = xmerge(g, 1);
           g = xmerge(g, 2);
           if (h == 0 && (l32 & 3) == 0) {
-            const int e = ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
-            float* o = p.gstat + (((size_t)t.n0 * p.gstat_E + e) * (p.cout / 4) + t.ct * 16 + nr * 8 + (l32 >> 2)) * 2;
+            const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
+            float* o = p.gstat + (((size_t)(t.n0 + wimg) * p.gstat_E + e) * (p.cout / 4) + t.ct * 16 + nr * 8 +
+                                  (l32 >> 2)) * 2;
             o[0] = g.mean;
             o[1] = g.m2;
           }
@@ -599,7 +613,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   const int ptid = tid - NP_T;
   XProducer<XF, SKIP, TW> P;
   P.init(ptid);
-  XSet s0, s1;
+  typename XProducer<XF, SKIP, TW>::Set s0, s1;
   // Lookahead cursor over the chunk stream: position jl = (unit ul, chunk kl of the unit), the
   // unit's tile decoded once per unit; past the end it stays on the last chunk (re-issued loads /
   // DMA of identical bytes keep the op counts fixed).
@@ -608,7 +622,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   int jl = 0, ul = 0, kl = 0, zl = 0;
   STile tl = unit_of(0, zl);
   int lastmain = 1, prevmain = 1;  // the last / the previous issued chunk is a 3x3 chunk
-  auto issue = [&](XSet& s) {  // DMA + register loads of the cursor's chunk, then advance
+  auto issue = [&](typename XProducer<XF, SKIP, TW>::Set& s) {  // DMA + register loads of the cursor's chunk, then advance
     const int c = __builtin_amdgcn_readfirstlane(zl * nchu + kl);
     prevmain = lastmain;
     lastmain = (!SKIP || c < nmain) ? 1 : 0;
@@ -626,17 +640,28 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     }
   };
   // Barrier once chunk q's DMA has landed, chunk q+1 being the last issued: younger are chunk q's
-  // register loads (10, none for a skip chunk), then all of chunk q+1 (9 + 10, or 5).
-  static_assert(X_LOADS_PER_CHUNK == 10 && XWDMA == XDMA3 && XDMA1 == 5, "barrier vmcnt literals");
+  // register loads (L = Geo::LOADS, none for a skip chunk), then all of chunk q+1 (9 + L, or 5).
+  static_assert(XWDMA == XDMA3 && XDMA1 == 5 && (Geo::LOADS == 10 || Geo::LOADS == 12), "barrier vmcnt literals");
   auto barrier = [&]() {
-    if (!SKIP || (prevmain && lastmain))
-      XBARRIER_PRODUCER(29);
-    else if (prevmain)
-      XBARRIER_PRODUCER(15);
-    else if (lastmain)
-      XBARRIER_PRODUCER(19);
-    else
-      XBARRIER_PRODUCER(5);
+    if constexpr (Geo::LOADS == 10) {
+      if (!SKIP || (prevmain && lastmain))
+        XBARRIER_PRODUCER(29);
+      else if (prevmain)
+        XBARRIER_PRODUCER(15);
+      else if (lastmain)
+        XBARRIER_PRODUCER(19);
+      else
+        XBARRIER_PRODUCER(5);
+    } else {
+      if (!SKIP || (prevmain && lastmain))
+        XBARRIER_PRODUCER(33);
+      else if (prevmain)
+        XBARRIER_PRODUCER(17);
+      else if (lastmain)
+        XBARRIER_PRODUCER(21);
+      else
+        XBARRIER_PRODUCER(5);
+    }
   };
   issue(s0);  // chunk 0
   const int main0 = lastmain;
@@ -710,8 +735,11 @@ static int launch_x3_tw(const ConvParams& p, int xform, hipStream_t stream) {
 // 1x1 skip segment.
 bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
   const int nch = p.cin_pad / 16 + (p.wskip ? p.cs_pad / 16 : 0);
-  return taps == 9 && xform != XF_DOWN && bn == XBN && p.bm == 256 && (p.TW == 32 || p.TW == 16) &&
-         p.TH * p.TW == 256 && p.IMGS == 1 && p.epi == EPI_NHWC && p.cout % XBN == 0 && p.cout_pad == p.cout &&
+  const bool one_img = (p.TW == 32 || p.TW == 16) && p.TH * p.TW == 256 && p.IMGS == 1;
+  const bool img8 = p.TW == 8 && p.TH == 8 && p.H == 8 && p.W == 8 && p.IMGS == 4 && p.N % 4 == 0 &&
+                    xform == XF_NONE && (!p.res || p.res_xform == XF_NONE);
+  return taps == 9 && xform != XF_DOWN && bn == XBN && p.bm == 256 && (one_img || img8) &&
+         p.epi == EPI_NHWC && p.cout % XBN == 0 && p.cout_pad == p.cout &&
          p.c0 % 16 == 0 && p.c1 % 16 == 0 && (!p.wskip || (p.sc0 % 16 == 0 && p.sc1 % 16 == 0 && p.sc0 < 4096 && p.sc1 < 4096)) &&
          p.ksplit >= 1 && nch % p.ksplit == 0 && (!p.res || p.res_xform != XF_DOWN || p.ksplit > 1);
 }
@@ -719,6 +747,7 @@ bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
 int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream) {
   if (p.TW == 32) return launch_x3_tw<32>(p, xform, stream);
   if (p.TW == 16) return launch_x3_tw<16>(p, xform, stream);
+  if (p.TW == 8) return launch_x3_tw<8>(p, xform, stream);
   return (int)hipErrorInvalidValue;
 }
 
