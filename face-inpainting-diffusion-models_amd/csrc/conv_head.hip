@@ -4,17 +4,18 @@
 //
 // Why not the MFMA conv kernels: cout = 6 (or 3) fills 6/32 of a 32-wide MFMA tile and the fp32
 // MFMA rate equals the fp32 VALU rate on gfx950 (MI355X_MICROARCH.md), so a GEMM tiling wastes
-// ~5x. Here each thread owns two vertically adjacent output pixels and keeps their 2 x 6
-// accumulators in registers; the weights are wave-uniform, so they arrive by scalar loads and
-// every MAC is one v_fma_f32 with an SGPR operand, each weight serving both pixels. Per 16-channel
-// chunk a block stages the activated 18 x 34 halo of its 16 x 32 tile in LDS (4 quad planes
-// [pixel][4 ch]: a wave's ds_read_b128 of 64 consecutive pixels is conflict-free); a thread reads
-// each halo column of 4 rows once for its 3 x 2 (tap row, pixel) uses. The next chunk's halo
-// loads are in flight in registers during the FMAs.
+// ~5x. Here each thread owns a column of 4 output pixels and keeps their 4 x 6 accumulators as
+// channel pairs; every MAC pair is one v_pk_fma_f32 (the input value broadcast to both halves,
+// two output channels' weights from a broadcast LDS read), the packed rate being the full fp32
+// VALU rate. Per 8-channel chunk a block stages the activated 34 x 34 halo of its 32 x 32 tile
+// (2 quad planes [pixel][4 ch]: a wave's ds_read_b128 of 64 consecutive pixels is conflict-free)
+// and the chunk's weights in LDS; a thread reads each halo column of 6 rows once for its
+// 3 x 4 (tap row, pixel) uses. The next chunk's halo loads are in flight in registers.
 //
 // Bound: VALU. Per output pixel 9 * cin * cout FMAs (13.8 kFLOP for cin 128, cout 6) against
 // ~0.6 KB of HBM traffic (4 * cin B of input + the step epilogue's 64 B): 23 FLOP/B, above the
-// 157 TF/s : 8 TB/s balance point of ~20 FLOP/B.
+// 157 TF/s : 8 TB/s balance point of ~20 FLOP/B. (The first version read the weights by scalar
+// loads: at 27 KB they miss the scalar cache and every wait exposed its latency, 39 TFLOP/s.)
 #include <hip/hip_runtime.h>
 
 #include "conv.h"
@@ -23,15 +24,21 @@
 namespace ifd {
 namespace {
 
-constexpr int HD_TW = 32, HD_TH = 16;                          // output tile (one image)
-constexpr int HD_HW = HD_TW + 2, HD_NP = HD_HW * (HD_TH + 2);  // 34 x 18 = 612 halo pixels
-constexpr int HD_NT = 256;                                     // one thread per 2 output pixels
-constexpr int HD_ITEMS = (HD_NP * 4 + HD_NT - 1) / HD_NT;      // (pixel, quad) items per thread: 10
+constexpr int HD_TW = 32, HD_TH = 32;                          // output tile (one image)
+constexpr int HD_HW = HD_TW + 2, HD_NP = HD_HW * (HD_TH + 2);  // 34 x 34 = 1156 halo pixels
+constexpr int HD_NT = 256;                                     // one thread per 4 output pixels
+constexpr int HD_PX = 4;                                       // pixels (rows) per thread
+constexpr int HD_CH = 8;                                       // channels per chunk
+constexpr int HD_ITEMS = (HD_NP * 2 + HD_NT - 1) / HD_NT;      // (pixel, quad) items per thread: 10
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// wh: [cin/16][9 taps][16 ci][8] fp32 (co 0..cout-1, zero padded), bias = p.bias
+// wh: [cin/8][9 taps][8 ci][8] fp32 (co 0..cout-1, zero padded), bias = p.bias
 template <int CO>
 __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const float* __restrict__ wh) {
-  __shared__ __attribute__((aligned(16))) float hal[4][HD_NP][4];  // quad plane q: [pixel][4 channels]
+  static_assert(CO % 2 == 0 || CO == 3, "channel pairs");
+  constexpr int CP = (CO + 1) / 2;                                 // output channel pairs
+  __shared__ __attribute__((aligned(16))) float hal[2][HD_NP][4];  // quad plane q: [pixel][4 channels]
+  __shared__ __attribute__((aligned(16))) float wl[9 * HD_CH * 8];  // the chunk's weights
   const int tid = threadIdx.x;
   const int tiles_x = p.W / HD_TW, tiles_y = p.H / HD_TH;
   int b = blockIdx.x;
@@ -41,38 +48,38 @@ __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const
   const int n = b / tiles_y;
   const int x0 = tx * HD_TW, y0 = ty * HD_TH;
   const int cin = p.c0;
-  const int nchunk = cin / 16;
+  const int nchunk = cin / HD_CH;
   const float* __restrict__ src = p.in0 + (size_t)n * p.H * p.W * cin;
 
-  // staging items: item i = (halo pixel i >> 2, channel quad i & 3); quad = tid & 3 for every item
-  const int q = tid & 3;
+  // staging items: item i = (halo pixel i >> 1, channel quad i & 1); quad = tid & 1 for every item
+  const int q = tid & 1;
   int goff[HD_ITEMS];
   bool inb[HD_ITEMS];
 #pragma unroll
   for (int k = 0; k < HD_ITEMS; ++k) {
     const int i = tid + k * HD_NT;
-    const int pix = i >> 2;
+    const int pix = i >> 1;
     const int hy = pix / HD_HW, hx = pix - hy * HD_HW;
     const int y = y0 + hy - 1, x = x0 + hx - 1;
-    inb[k] = i < 4 * HD_NP && y >= 0 && y < p.H && x >= 0 && x < p.W;
+    inb[k] = i < 2 * HD_NP && y >= 0 && y < p.H && x >= 0 && x < p.W;
     goff[k] = inb[k] ? (y * p.W + x) * cin + 4 * q : 0;
   }
   f32x4 raw[HD_ITEMS];
   auto load = [&](int ch) {
 #pragma unroll
     for (int k = 0; k < HD_ITEMS; ++k)
-      raw[k] = inb[k] ? gld4(src + goff[k] + 16 * ch) : f32x4{0.f, 0.f, 0.f, 0.f};
+      raw[k] = inb[k] ? gld4(src + goff[k] + HD_CH * ch) : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   auto stage = [&](int ch) {
     f32x4 ca = {1.f, 1.f, 1.f, 1.f}, cb = {0.f, 0.f, 0.f, 0.f};
     if (p.act != ACT_NONE) {
-      ca = gld4(p.actA + (size_t)n * cin + 16 * ch + 4 * q);
-      cb = gld4(p.actB + (size_t)n * cin + 16 * ch + 4 * q);
+      ca = gld4(p.actA + (size_t)n * cin + HD_CH * ch + 4 * q);
+      cb = gld4(p.actB + (size_t)n * cin + HD_CH * ch + 4 * q);
     }
 #pragma unroll
     for (int k = 0; k < HD_ITEMS; ++k) {
       const int i = tid + k * HD_NT;
-      if (i < 4 * HD_NP) {
+      if (i < 2 * HD_NP) {
         f32x4 v;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -83,16 +90,20 @@ __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const
           }
           v[c] = inb[k] ? t : 0.f;  // zero padding of the activated input
         }
-        *(f32x4*)&hal[q][i >> 2][0] = v;
+        *(f32x4*)&hal[q][i >> 1][0] = v;
       }
     }
+    for (int i = tid; i < 9 * HD_CH * 2; i += HD_NT)  // 576 weights as float4
+      *(f32x4*)&wl[4 * i] = gld4(wh + (size_t)ch * 9 * HD_CH * 8 + 4 * i);
   };
 
-  const int py = 2 * (tid / HD_TW), px = tid % HD_TW;  // pixels (py, px) and (py + 1, px)
-  const int hp = py * HD_HW + px;                      // halo pixel of tap (0, 0) of the first
-  float acc[2][CO];
+  const int px = tid % HD_TW, py = HD_PX * (tid / HD_TW);  // pixels (py .. py + 3, px)
+  const int hp = py * HD_HW + px;                           // halo pixel of tap (0, 0) of the first
+  f32x2 acc[HD_PX][CP];
 #pragma unroll
-  for (int c = 0; c < CO; ++c) acc[0][c] = acc[1][c] = 0.f;
+  for (int r = 0; r < HD_PX; ++r)
+#pragma unroll
+    for (int c = 0; c < CP; ++c) acc[r][c] = f32x2{0.f, 0.f};
 
   load(0);
   for (int ch = 0; ch < nchunk; ++ch) {
@@ -100,23 +111,28 @@ __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const
     stage(ch);
     __syncthreads();
     if (ch + 1 < nchunk) load(ch + 1);  // in flight during this chunk's FMAs
-    const float* __restrict__ w = wh + (size_t)ch * 9 * 16 * 8;
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        f32x4 v[4];  // halo rows py .. py + 3 of column px + dx
+      for (int qq = 0; qq < 2; ++qq) {
+        f32x4 v[HD_PX + 2];  // halo rows py .. py + 5 of column px + dx
 #pragma unroll
-        for (int hr = 0; hr < 4; ++hr) v[hr] = *(const f32x4*)&hal[qq][hp + hr * HD_HW + dx][0];
+        for (int hr = 0; hr < HD_PX + 2; ++hr) v[hr] = *(const f32x4*)&hal[qq][hp + hr * HD_HW + dx][0];
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
           for (int dy = 0; dy < 3; ++dy) {
-            const float* wr = w + ((dy * 3 + dx) * 16 + 4 * qq + c) * 8;
+            const float* wr = wl + ((dy * 3 + dx) * HD_CH + 4 * qq + c) * 8;
+            const f32x4 w03 = *(const f32x4*)wr;
+            const f32x4 w47 = *(const f32x4*)(wr + 4);
+            const f32x2 wp[4] = {f32x2{w03[0], w03[1]}, f32x2{w03[2], w03[3]}, f32x2{w47[0], w47[1]},
+                                 f32x2{w47[2], w47[3]}};
 #pragma unroll
-            for (int co = 0; co < CO; ++co) {
-              acc[0][co] = __builtin_fmaf(v[dy][c], wr[co], acc[0][co]);
-              acc[1][co] = __builtin_fmaf(v[dy + 1][c], wr[co], acc[1][co]);
+            for (int r = 0; r < HD_PX; ++r) {
+              const float x = v[dy + r][c];
+#pragma unroll
+              for (int cp = 0; cp < CP; ++cp)
+                acc[r][cp] = __builtin_elementwise_fma(f32x2{x, x}, wp[cp], acc[r][cp]);
             }
           }
       }
@@ -126,32 +142,38 @@ __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const
   // epilogue (conv.hip's NCHW / DDIM / DDPM paths)
   const int HWp = p.H * p.W;
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-  const size_t pix = (size_t)(y0 + py + r) * p.W + (x0 + px);
-  if (p.epi == EPI_NCHW) {
+  for (int r = 0; r < HD_PX; ++r) {
+    float a[2 * CP];
 #pragma unroll
-    for (int co = 0; co < CO; ++co) p.out[((size_t)n * CO + co) * HWp + pix] = acc[r][co] + p.bias[co];
-    continue;
-  }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const size_t o3 = ((size_t)n * 3 + c) * HWp + pix;
-    const size_t om = (size_t)n * HWp + pix;
-    const float eps = acc[r][c] + p.bias[c];
-    const float x = p.img[o3];
-    const float mk = p.sc.inject ? p.mask[om] : 0.f;
-    const float g = p.sc.inject ? p.gt[o3] : 0.f;
-    const float kn = p.sc.inject ? p.known[o3] : 0.f;
-    float v;
-    if (p.epi == EPI_DDIM) {
-      const float nz = p.sc.use_noise ? p.noise[o3] : 0.f;
-      v = ddim_step_value(p.sc, x, eps, nz, g, mk, kn);
-    } else {
-      const float var_v = acc[r][CO > 3 ? c + 3 : c] + p.bias[c + 3];
-      v = ddpm_step_value(p.sc, x, eps, var_v, p.noise[o3], g, mk, kn);
+    for (int cp = 0; cp < CP; ++cp) {
+      a[2 * cp] = acc[r][cp][0];
+      a[2 * cp + 1] = acc[r][cp][1];
     }
-    p.img[o3] = v;
-  }
+    const size_t pix = (size_t)(y0 + py + r) * p.W + (x0 + px);
+    if (p.epi == EPI_NCHW) {
+#pragma unroll
+      for (int co = 0; co < CO; ++co) p.out[((size_t)n * CO + co) * HWp + pix] = a[co] + p.bias[co];
+      continue;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const size_t o3 = ((size_t)n * 3 + c) * HWp + pix;
+      const size_t om = (size_t)n * HWp + pix;
+      const float eps = a[c] + p.bias[c];
+      const float x = p.img[o3];
+      const float mk = p.sc.inject ? p.mask[om] : 0.f;
+      const float g = p.sc.inject ? p.gt[o3] : 0.f;
+      const float kn = p.sc.inject ? p.known[o3] : 0.f;
+      float v;
+      if (p.epi == EPI_DDIM) {
+        const float nz = p.sc.use_noise ? p.noise[o3] : 0.f;
+        v = ddim_step_value(p.sc, x, eps, nz, g, mk, kn);
+      } else {
+        const float var_v = a[CO > 3 ? c + 3 : c] + p.bias[c + 3];
+        v = ddpm_step_value(p.sc, x, eps, var_v, p.noise[o3], g, mk, kn);
+      }
+      p.img[o3] = v;
+    }
   }
 }
 
@@ -159,21 +181,21 @@ __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const
 
 bool conv_head_eligible(const ConvParams& p, int taps, int xform) {
   const bool step = p.epi == EPI_DDIM || p.epi == EPI_DDPM;
-  return taps == 9 && xform == XF_NONE && !p.in1 && p.c1 == 0 && p.c0 % 16 == 0 && p.c0 >= 16 && !p.wskip &&
+  return taps == 9 && xform == XF_NONE && !p.in1 && p.c1 == 0 && p.c0 % HD_CH == 0 && p.c0 >= HD_CH && !p.wskip &&
          !p.res && (p.epi == EPI_NCHW || step) && (p.cout == 6 || (p.cout == 3 && p.epi != EPI_DDPM)) &&
          p.H % HD_TH == 0 && p.W % HD_TW == 0 && p.Hin == p.H && p.Win == p.W;
 }
 
-size_t conv_head_pack_floats(int cin) { return (size_t)(cin / 16) * 9 * 16 * 8; }
+size_t conv_head_pack_floats(int cin) { return (size_t)(cin / HD_CH) * 9 * HD_CH * 8; }
 
-// w: torch layout [cout][cin][3][3] -> [cin/16][tap][16][8]
+// w: torch layout [cout][cin][3][3] -> [cin/8][tap][8][8]
 void conv_head_pack(const float* w, int cout, int cin, float* dst) {
-  for (int ch = 0; ch < cin / 16; ++ch)
+  for (int ch = 0; ch < cin / HD_CH; ++ch)
     for (int tap = 0; tap < 9; ++tap)
-      for (int c = 0; c < 16; ++c)
+      for (int c = 0; c < HD_CH; ++c)
         for (int co = 0; co < 8; ++co)
-          dst[((size_t)(ch * 9 + tap) * 16 + c) * 8 + co] =
-              co < cout ? w[((size_t)co * cin + ch * 16 + c) * 9 + tap] : 0.f;
+          dst[((size_t)(ch * 9 + tap) * HD_CH + c) * 8 + co] =
+              co < cout ? w[((size_t)co * cin + ch * HD_CH + c) * 9 + tap] : 0.f;
 }
 
 int launch_conv_head(const ConvParams& p, const float* wh, hipStream_t stream) {
