@@ -24,8 +24,9 @@ void launch_step(int mode, const StepCoeffs& sc, const float* out6, float* img, 
 // act + AvgPool2d(2,2) of an NHWC tensor (the down-ResBlock's h_upd, code/nn.py:190-195) for the
 // split-precision conv, which has no avg-pool prologue: out[n, y, x, c] = ((a00 + a01) + a10) + a11) / 4
 // with a = act(A[n,c] v + B[n,c]), the arithmetic of conv.hip's XF_DOWN prologue.
+// out_raw (optional): also pool(x) without the act, from the same reads (the block's residual)
 int launch_act_pool(const float* x, int C, int N, int Hin, int act, const float* A, const float* B, float* out,
-                    hipStream_t s);
+                    float* out_raw, hipStream_t s);
 void launch_blend(const float* res, const float* gt, const float* mask, float* out, int N, int C, int HW,
                   hipStream_t s);
 

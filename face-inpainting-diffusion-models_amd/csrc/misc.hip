@@ -390,7 +390,7 @@ void launch_blend(const float* res, const float* gt, const float* mask, float* o
 // act + 2x2 average pool, 4 channels per thread (16-byte loads/stores, coalesced along C).
 __global__ __launch_bounds__(256) void act_pool_kernel(const float* __restrict__ x, int C, int N, int Hin, int act,
                                                        const float* __restrict__ A, const float* __restrict__ B,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ out, float* __restrict__ out_raw) {
   const int Ho = Hin / 2, Q = C / 4;
   const size_t tot = (size_t)N * Ho * Ho * Q;
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -421,13 +421,25 @@ __global__ __launch_bounds__(256) void act_pool_kernel(const float* __restrict__
     r[j] = s * 0.25f;
   }
   *(f32x4*)(out + pix * C + 4 * q) = r;
+  if (out_raw) {  // the down-ResBlock's residual pool(x) from the same four reads
+    f32x4 rr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = v00[j];
+      s = s + v01[j];
+      s = s + v10[j];
+      s = s + v11[j];
+      rr[j] = s * 0.25f;
+    }
+    *(f32x4*)(out_raw + pix * C + 4 * q) = rr;
+  }
 }
 
 int launch_act_pool(const float* x, int C, int N, int Hin, int act, const float* A, const float* B, float* out,
-                    hipStream_t s) {
+                    float* out_raw, hipStream_t s) {
   const size_t tot = (size_t)N * (Hin / 2) * (Hin / 2) * (C / 4);
   hipLaunchKernelGGL(act_pool_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, x, C, N, Hin, act, A, B,
-                     out);
+                     out, out_raw);
   return (int)hipGetLastError();
 }
 

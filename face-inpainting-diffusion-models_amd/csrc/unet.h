@@ -148,6 +148,7 @@ class Model {
   std::map<const float*, float*> stat_area_;
   std::map<const float*, StatRec> stat_;
   bool gn_fused_ = true;
+  const float* pooled_raw_ = nullptr;  // tensor whose raw 2x2 pool sits in o_pool2_ (act_pool)
   int prec_ = 0;
 };
 

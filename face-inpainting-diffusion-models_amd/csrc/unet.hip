@@ -613,8 +613,16 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
       hipEvent_t pe;
       prof_begin(s, &pe, "act_pool");
       int e = 0;
-      if (pool_in) e = launch_act_pool(in0, c0, N, Hin, act, A, Bc, ws_ + o_pool_, s);
-      if (!e && pool_res) e = launch_act_pool(res, cw.cout, N, resH, ACT_NONE, nullptr, nullptr, ws_ + o_pool2_, s);
+      // conv1 of a down-ResBlock also pools its raw input for conv2's residual (same tensor, read
+      // once); conv2 then finds pool(res) already in o_pool2_
+      if (pool_in) {
+        const bool raw_too = c0 == cw.cout;  // a down-ResBlock keeps its width: conv2's residual is in0
+        e = launch_act_pool(in0, c0, N, Hin, act, A, Bc, ws_ + o_pool_, raw_too ? ws_ + o_pool2_ : nullptr, s);
+        pooled_raw_ = raw_too ? in0 : nullptr;
+      }
+      if (!e && pool_res && res != pooled_raw_)
+        e = launch_act_pool(res, cw.cout, N, resH, ACT_NONE, nullptr, nullptr, ws_ + o_pool2_, nullptr, s);
+      if (pool_res) pooled_raw_ = nullptr;
       prof_end(s, pe, "act_pool", 0.0, 4.0 * N * (double)Hin * Hin * (c0 + (pool_res ? cw.cout : 0)) * 1.25);
       IFD_REQUIRE(e == 0, "act_pool launch");
       p = q;
@@ -840,6 +848,7 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   const int mc = cfg_.model_channels;
   float* x0 = ws_ + o_x0_;
   stat_.clear();
+  pooled_raw_ = nullptr;
   {
     const char* gf = getenv("IFD_GN_FUSED");  // development switch: 0 = separate statistics pass
     gn_fused_ = !(gf && gf[0] == '0');
