@@ -103,27 +103,38 @@ struct XDec {
   int lks, lnct, ltx, lty, limg;
   bool xcd;        // conv.hip's XCD-aware map (pixel tiles in groups of 8)
   bool blk_major;  // a block's consecutive units = the channel tiles of one pixel tile
+  int nct;         // channel tiles; not a power of two (the 1536-wide qkv 1x1): decoded by division
+  bool pow2;
 };
 __device__ __forceinline__ XDec x3_dec(const ConvParams& p, int nct) {
+  const bool pow2 = (nct & (nct - 1)) == 0;
   return {__builtin_ctz(p.ksplit), __builtin_ctz(nct), __builtin_ctz(p.tiles_x), __builtin_ctz(p.tiles_y),
-          __builtin_ctz(p.IMGS), p.npix_tiles % 8 == 0, p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0};
+          __builtin_ctz(p.IMGS), pow2 && p.npix_tiles % 8 == 0, p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0,
+          nct, pow2};
 }
 // Unit u of block b. blk_major (no split-K, pixel tiles a multiple of the grid): block b takes
 // pixel tiles b, b + G, ... and runs all channel tiles of each back to back, so the second
 // channel tile re-reads the same input (3x3 halo and skip operand) from L2 instead of HBM.
 // Otherwise L = b + u G walks the XCD-aware map (S splits of a tile consecutive in L).
+// NP2: non-power-of-two channel-tile counts allowed (the 1x1-only launches, which use the SKIP
+// instantiations; the others keep the shift-only decode and its register budget)
+template <bool NP2>
 __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int b, int u, int& z) {
   STile t;
   int bx;
   if (d.blk_major) {
     z = 0;
-    t.ct = u & ((1 << d.lnct) - 1);
-    bx = b + (int)gridDim.x * (u >> d.lnct);
+    const int uq = (!NP2 || d.pow2) ? u >> d.lnct : u / d.nct;
+    t.ct = u - uq * d.nct;
+    bx = b + (int)gridDim.x * uq;
   } else {
     const int L = b + u * (int)gridDim.x;
     z = L & ((1 << d.lks) - 1);
     const int v = L >> d.lks;
-    if (d.xcd) {
+    if (NP2 && !d.pow2) {
+      bx = v / d.nct;
+      t.ct = v - bx * d.nct;
+    } else if (d.xcd) {
       const int rr = v & ((8 << d.lnct) - 1);
       t.ct = rr >> 3;
       bx = ((v >> (3 + d.lnct)) << 3) + (rr & 7);
@@ -437,7 +448,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   const int nchu = (nmain + nskip) / S;  // chunks per unit (host: divisible)
   const int J = nu * nchu;
   const XDec dec = x3_dec(p, nct);
-  auto unit_of = [&](int u, int& z) { return x3_unit(p, dec, (int)blockIdx.x, u, z); };
+  auto unit_of = [&](int u, int& z) { return x3_unit<SKIP>(p, dec, (int)blockIdx.x, u, z); };
 
   if (consumer) {
     const int h = lane >> 5, l32 = lane & 31;
@@ -738,7 +749,8 @@ bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
   const bool one_img = (p.TW == 32 || p.TW == 16) && p.TH * p.TW == 256 && p.IMGS == 1;
   const bool img8 = p.TW == 8 && p.TH == 8 && p.H == 8 && p.W == 8 && p.IMGS == 4 && p.N % 4 == 0 &&
                     xform == XF_NONE && (!p.res || p.res_xform == XF_NONE);
-  return taps == 9 && xform != XF_DOWN && bn == XBN && p.bm == 256 && (one_img || img8) &&
+  const bool only1x1 = taps == 1 && p.cin_pad == 0 && p.wskip;  // a 1x1 conv: 1x1 chunks only
+  return (taps == 9 || only1x1) && xform != XF_DOWN && bn == XBN && p.bm == 256 && (one_img || img8) &&
          p.epi == EPI_NHWC && p.cout % XBN == 0 && p.cout_pad == p.cout &&
          p.c0 % 16 == 0 && p.c1 % 16 == 0 && (!p.wskip || (p.sc0 % 16 == 0 && p.sc1 % 16 == 0 && p.sc0 < 4096 && p.sc1 < 4096)) &&
          p.ksplit >= 1 && nch % p.ksplit == 0 && (!p.res || p.res_xform != XF_DOWN || p.ksplit > 1);

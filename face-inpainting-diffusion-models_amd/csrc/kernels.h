@@ -24,6 +24,9 @@ void launch_step(int mode, const StepCoeffs& sc, const float* out6, float* img, 
 // act + AvgPool2d(2,2) of an NHWC tensor (the down-ResBlock's h_upd, code/nn.py:190-195) for the
 // split-precision conv, which has no avg-pool prologue: out[n, y, x, c] = ((a00 + a01) + a10) + a11) / 4
 // with a = act(A[n,c] v + B[n,c]), the arithmetic of conv.hip's XF_DOWN prologue.
+// act(A x + B) of an NHWC tensor (no pooling): the split kernel's 1x1 operand
+int launch_act_apply(const float* x, int C, int N, int HW, int act, const float* A, const float* B, float* out,
+                     hipStream_t s);
 // out_raw (optional): also pool(x) without the act, from the same reads (the block's residual)
 int launch_act_pool(const float* x, int C, int N, int Hin, int act, const float* A, const float* B, float* out,
                     float* out_raw, hipStream_t s);

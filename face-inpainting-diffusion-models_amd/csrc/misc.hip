@@ -435,6 +435,35 @@ __global__ __launch_bounds__(256) void act_pool_kernel(const float* __restrict__
   }
 }
 
+// act(A[n,c] x + B[n,c]) of an NHWC tensor, materialised for the split kernel's 1x1 chunks (the
+// attention qkv conv's GroupNorm prologue): the arithmetic of the conv prologues.
+__global__ __launch_bounds__(256) void act_apply_kernel(const float* __restrict__ x, int C, int HW, int act,
+                                                        const float* __restrict__ A, const float* __restrict__ B,
+                                                        size_t tot, float* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int Q = C / 4;
+  const int q = (int)(i % Q);
+  const int n = (int)(i / ((size_t)Q * HW));
+  const f32x4 v = *(const f32x4*)(x + 4 * i);
+  const f32x4 a = *(const f32x4*)(A + (size_t)n * C + 4 * q), c = *(const f32x4*)(B + (size_t)n * C + 4 * q);
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float t = a[j] * v[j] + c[j];
+    r[j] = act == ACT_AFFINE_SILU ? silu_fast(t) : t;
+  }
+  *(f32x4*)(out + 4 * i) = r;
+}
+
+int launch_act_apply(const float* x, int C, int N, int HW, int act, const float* A, const float* B, float* out,
+                     hipStream_t s) {
+  const size_t tot = (size_t)N * HW * (C / 4);
+  hipLaunchKernelGGL(act_apply_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, x, C, HW, act, A, B, tot,
+                     out);
+  return (int)hipGetLastError();
+}
+
 int launch_act_pool(const float* x, int C, int N, int Hin, int act, const float* A, const float* B, float* out,
                     float* out_raw, hipStream_t s) {
   const size_t tot = (size_t)N * (Hin / 2) * (Hin / 2) * (C / 4);

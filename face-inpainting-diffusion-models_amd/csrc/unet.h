@@ -142,6 +142,7 @@ class Model {
   size_t o_x0_ = 0, o_bufs_[3] = {0, 0, 0}, o_t1_ = 0, o_qkv_ = 0, o_ao_ = 0, o_A_ = 0, o_B_ = 0, o_part_ = 0,
          o_emb_ = 0, o_h1_ = 0, o_E_ = 0, o_split_ = 0, o_pool_ = 0, o_pool2_ = 0;
   size_t split_floats_ = 0;
+  size_t pool_floats_ = 0;
   std::vector<size_t> o_hs_;
   // GroupNorm granule statistics: one area per activation buffer (hs, bufs, t1); stat_ holds the
   // buffers whose current contents have valid statistics (reset per forward)

@@ -344,6 +344,8 @@ int Model::finalize() {
     if (c.taps == 9 && c.bn == 64 && c.cin_pad % 16 == 0 && (!c.has_skip || c.cs_pad % 16 == 0)) {
       c.x3_off = reserve((size_t)c.cout_pad * c.cin_pad * c.taps);
       if (c.has_skip) c.x3s_off = reserve((size_t)c.cout_pad * c.cs_pad);
+    } else if (c.taps == 1 && c.bn == 64 && c.cin_pad % 16 == 0 && !c.has_skip) {
+      c.x3s_off = reserve((size_t)c.cout_pad * c.cin_pad);  // a 1x1 conv runs as 1x1 chunks only
     }
   };
   auto plan_gn = [&](GNW& g) {
@@ -382,6 +384,8 @@ int Model::finalize() {
     pack_conv(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob, c.w_off);
     c.x3_ok = c.x3_off && pack_conv_x3(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob,
                                        c.x3_off);
+    if (c.taps == 1 && c.x3s_off)
+      c.x3_ok = pack_conv_x3(host_[c.wname], c.cout, c.cin, 1, c.bn, c.cin_pad, c.cout_pad, blob, c.x3s_off);
     if (c.x3_ok && c.has_skip)
       c.x3_ok = pack_conv_x3(host_[c.swname], c.cout, c.cs, 1, c.bn, c.cs_pad, c.cout_pad, blob, c.x3s_off);
     const auto& b = host_[c.bname];
@@ -530,6 +534,14 @@ int Model::ensure_workspace(int B) {
     for (auto& L : blk)
       if (L.kind == L_RES && res_[L.idx].xf == XF_DOWN)
         maxpool = std::max(maxpool, (size_t)B * (L.res_in / 2) * (L.res_in / 2) * res_[L.idx].cin);
+  // ... and act(GN(x)) of the attention blocks' qkv conv (B x res^2 x C)
+  for (auto* blocks : {&in_blocks_, &out_blocks_})
+    for (auto& blk : *blocks)
+      for (auto& L : blk)
+        if (L.kind == L_ATTN) maxpool = std::max(maxpool, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C);
+  for (auto& L : mid_)
+    if (L.kind == L_ATTN) maxpool = std::max(maxpool, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C);
+  pool_floats_ = maxpool;
   o_pool_ = reserve(maxpool);
   o_pool2_ = reserve(maxpool);  // pooled residual (a down-ResBlock keeps cin == cout)
   o_emb_ = reserve((size_t)B * emb_dim_);
@@ -592,6 +604,28 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   // persistent workgroup per CU, 2 two persistent workgroups per CU (conv_stream.hip)
   const char* st_env = getenv("IFD_CONV_STREAM");
   const int stream_mode = st_env ? atoi(st_env) : kDefaultStreamMode;
+  // 3xf16 1x1 conv (attention qkv / proj_out): the split kernel's 1x1 chunks over the raw operand,
+  // act(GN(x)) materialised first when the conv has a prologue (act_apply, the conv prologue's
+  // fp32 arithmetic)
+  if (prec_ == IFD_PREC_3XF16 && cw.taps == 1 && cw.x3_ok && cw.x3s_off && epi == EPI_NHWC && !in1 &&
+      xf == XF_NONE) {
+    ConvParams q = p;
+    q.in0 = nullptr; q.c0 = 0; q.in1 = nullptr; q.c1 = 0; q.cin_pad = 0; q.act = ACT_NONE;
+    q.s0 = act != ACT_NONE ? ws_ + o_pool_ : in0; q.sc0 = c0; q.s1 = nullptr; q.sc1 = 0;
+    q.wskip = wblob_ + cw.x3s_off; q.cs_pad = cw.cin_pad;
+    if (conv_x3_eligible(q, 1, XF_NONE, cw.bn)) {
+      if (act != ACT_NONE) {
+        IFD_REQUIRE((size_t)N * H * H * c0 <= pool_floats_, "act_apply workspace");
+        hipEvent_t pe;
+        prof_begin(s, &pe, "act_pool");
+        const int e = launch_act_apply(in0, c0, N, H * H, act, A, Bc, ws_ + o_pool_, s);
+        prof_end(s, pe, "act_pool", 0.0, 8.0 * N * (double)H * H * c0);
+        IFD_REQUIRE(e == 0, "act_apply launch");
+      }
+      p = q;
+      act = ACT_NONE;
+    }
+  }
   // 3xf16: the split kernel has no avg-pool prologue or residual; a down-ResBlock's convs read
   // act+pool(x) / pool(x) materialised by act_pool at the output resolution instead (the same
   // fp32 arithmetic as conv.hip's XF_DOWN paths)
