@@ -75,7 +75,7 @@ struct ConvParams {
   StepCoeffs sc;
   // IFD_TRACE builds only: per-block timestamps (see conv.hip / conv_stream.hip)
   unsigned long long* trace;
-  // optional GroupNorm granule statistics of the output (norm.hip): gstat[n][e][cout/4] =
+  // optional GroupNorm granule statistics of the output (norm.hip): gstat[n][cout/4][e] =
   // (mean, M2); e = the tile's index within its image (x4 + consumer wave in conv_stream2).
   // Written only for single-image tiles without split-K (the host checks).
   float* gstat;

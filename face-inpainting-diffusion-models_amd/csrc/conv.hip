@@ -435,7 +435,7 @@ __global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvPar
             a = gmerge(a, GStat{tile[o], tile[o + 1], tile[o + 2]});
           }
           const int e = ty * p.tiles_x + tx;
-          float* o = p.gstat + (((size_t)n0 * p.gstat_E + e) * (p.cout / 4) + ct * QPP + tid) * 2;
+          float* o = p.gstat + (((size_t)n0 * (p.cout / 4) + ct * QPP + tid) * p.gstat_E + e) * 2;
           o[0] = a.mean;
           o[1] = a.m2;
         }
@@ -632,10 +632,10 @@ __global__ void splitk_reduce_kernel(ConvParams p) {
 // summed in slab order, + bias, + residual - splitk_reduce_kernel's arithmetic - stored, and folded
 // into shifted sums (K = the lane's first value); the quad's 4 channels and the 4 pixel lanes merge
 // in a fixed order (Chan) into granule entry (n, slice) of the quad: the entry layout of the conv
-// epilogues (gstat[n][e][cout/4] = (mean, M2), e = slice, cnt = 4 * SKG_SL values). 16 quads x
-// 16 pixel lanes per block: enough blocks even for the 8x8 layers (one slice per image).
+// epilogues (gstat[n][cout/4][e] = (mean, M2), e = slice, cnt = 4 * SKG_SL values). 8 quads x
+// 32 pixel lanes per block: enough blocks even for the 8x8 layers (one slice per image).
 constexpr int SKG_SL = 64;
-constexpr int SKG_Q = 16, SKG_PL = 256 / SKG_Q;
+constexpr int SKG_Q = 8, SKG_PL = 256 / SKG_Q;
 __global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
   __shared__ float red[SKG_PL][SKG_Q][3];
   const int q = threadIdx.x % SKG_Q, pl = threadIdx.x / SKG_Q;
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
     GStat a = {red[0][q][0], red[0][q][1], red[0][q][2]};
     for (int l = 1; l < SKG_PL; ++l)
       if (red[l][q][0] > 0.f) a = gmerge(a, GStat{red[l][q][0], red[l][q][1], red[l][q][2]});
-    float* o = p.gstat + (((size_t)n * (HW / slice) + e) * QP + qq) * 2;
+    float* o = p.gstat + (((size_t)n * QP + qq) * (HW / slice) + e) * 2;
     o[0] = a.mean;
     o[1] = a.m2;
   }

@@ -523,7 +523,7 @@ __global__ __launch_bounds__(NT, 4) void conv_stream2_kernel(ConvParams p) {
         gs = gstat_xlanes16(gs);
         if (lane < 16) {
           const int e = ((t.y0 / STH) * p.tiles_x + t.x0 / STW) * 4 + wave;
-          float* o = p.gstat + (((size_t)t.n0 * p.gstat_E + e) * (p.cout / 4) + t.ct * 16 + q) * 2;
+          float* o = p.gstat + (((size_t)t.n0 * (p.cout / 4) + t.ct * 16 + q) * p.gstat_E + e) * 2;
           o[0] = gs.mean;
           o[1] = gs.m2;
         }

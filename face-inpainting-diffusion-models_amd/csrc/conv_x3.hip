@@ -579,8 +579,8 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           g = xmerge(g, 2);
           if (h == 0 && (l32 & 3) == 0) {
             const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
-            float* o = p.gstat + (((size_t)(t.n0 + wimg) * p.gstat_E + e) * (p.cout / 4) + t.ct * 16 + nr * 8 +
-                                  (l32 >> 2)) * 2;
+            float* o = p.gstat + (((size_t)(t.n0 + wimg) * (p.cout / 4) + t.ct * 16 + nr * 8 + (l32 >> 2)) *
+                                      p.gstat_E + e) * 2;
             o[0] = g.mean;
             o[1] = g.m2;
           }

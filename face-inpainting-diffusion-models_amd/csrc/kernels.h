@@ -7,7 +7,7 @@ namespace ifd {
 int gn_slices(int HW, int* slice);
 int launch_gn(const float* p0, int c0, const float* p1, int c1, int N, int HW, const float* gamma, const float* beta,
               const float* emb, int emb_stride, int emb_off, float* part, float* A, float* B, hipStream_t stream);
-// granule statistics (norm.hip): P[N][E][C/4][2] = (mean, M2) over `cnt` values per entry
+// granule statistics (norm.hip): P[N][C/4][E][2] = (mean, M2) over `cnt` values per entry
 int launch_gn_granules(const float* x, int C, int N, int HW, float* part, int* E, float* cnt, hipStream_t stream);
 int launch_gn_finalize2(const float* part0, int E0, float cnt0, int C0, const float* part1, int E1, float cnt1,
                         int C1, int N, const float* gamma, const float* beta, const float* emb, int emb_stride,

@@ -191,7 +191,7 @@ int launch_gn(const float* p0, int c0, const float* p1, int c1, int N, int HW, c
 
 // ---------------------------------------------------------------------------------------------
 // Granule statistics. Every activation tensor can carry per-(image, entry, channel quad)
-// partial statistics P[n][e][c/4] = (mean, M2) over `cnt` values (an entry = a fixed set of
+// partial statistics P[n][c/4][e] = (mean, M2) over `cnt` values (an entry = a fixed set of
 // pixels, the same for all granules). The convs that PRODUCE a tensor write them from their
 // epilogue (conv.hip / conv_stream.hip, ConvParams::gstat), so the GroupNorm of the next layer
 // needs no pass over the tensor; tensors without them get gn_granules_kernel (one streaming pass).
@@ -203,7 +203,7 @@ struct GnGranuleParams {
   int HW;         // pixels per image
   int slice;      // pixels per entry (block)
   int E;          // entries per image
-  float* part;    // [N][E][C/4][2]
+  float* part;    // [N][C/4][E][2]
 };
 
 // one block per (entry, n): thread layout as gn_partial_kernel (channel quad x pixel lane),
@@ -250,14 +250,14 @@ __global__ __launch_bounds__(GN_NT) void gn_granules_kernel(GnGranuleParams p) {
       const int o = (l * QPT + qq) * 3;
       a = merge(a, Stat{red[o], red[o + 1], red[o + 2]});
     }
-    float* o = p.part + (((size_t)n * p.E + s) * QPT + qq) * 2;
+    float* o = p.part + (((size_t)n * QPT + qq) * p.E + s) * 2;
     o[0] = a.mean;
     o[1] = a.m2;
   }
 }
 
 struct GnSrc {
-  const float* part;  // [N][E][C/4][2]
+  const float* part;  // [N][C/4][E][2]
   int E, C;
   float cnt;          // values per (entry, granule)
 };
@@ -303,8 +303,8 @@ __global__ __launch_bounds__(GN_NT) void gn_finalize2_kernel(GnFinalize2Params p
       const GnSrc& S = first ? p.s0 : p.s1;
       const int gr = (first ? c : c - p.s0.C) >> 2;
       const int QP = S.C >> 2;
-      const float* base = S.part + ((size_t)n * S.E * QP + gr) * 2;
-      for (int e = tid; e < S.E; e += GN_NT) f(base + (size_t)e * QP * 2, (double)S.cnt);
+      const float* base = S.part + ((size_t)n * QP + gr) * S.E * 2;  // the granule's entries, contiguous
+      for (int e = tid; e < S.E; e += GN_NT) f(base + (size_t)e * 2, (double)S.cnt);
     }
   };
   double sn = 0.0, sm = 0.0;
