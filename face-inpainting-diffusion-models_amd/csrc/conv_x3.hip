@@ -163,6 +163,8 @@ struct XProducer {
   static constexpr int IT = Geo::ITEMS;
   using Set = XSet<IT>;
   int ptid, hh;  // hh: channel half (8 of the chunk's 16 channels) this thread stages
+  int pimg;      // four-image tiles: the image of the tile this thread stages (= its wave): one
+                 // image per thread, so one set of GroupNorm coefficients per thread
   int lane16;    // 16 * lane: the weight DMA's per-lane byte offset
   int hi[IT], hy[IT], hx[IT], ldso[IT];  // image of the tile, halo row / column; ldso: 16-B slot of
                                          // the pixel in the hi plane, -1 unused
@@ -183,14 +185,22 @@ struct XProducer {
     ptid = t;
     hh = t & 1;
     lane16 = 16 * (t & 63);
+    pimg = Geo::IMG > 1 ? t >> 6 : 0;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int idx = t + i * NP_T, pix = idx >> 1;
-      hi[i] = pix / Geo::HP;
-      const int rem = pix - hi[i] * Geo::HP;
-      hy[i] = rem / Geo::HW;
-      hx[i] = rem - hy[i] * Geo::HW;
-      ldso[i] = idx < 2 * Geo::NP ? hh * Geo::NP + pix : -1;
+      if (Geo::IMG > 1) {  // items (lane + 64 i) of the wave's image: 2 x 100 per image
+        const int idx = (t & 63) + 64 * i, pix = idx >> 1;
+        hi[i] = pimg;
+        hy[i] = pix / Geo::HW;
+        hx[i] = pix - hy[i] * Geo::HW;
+        ldso[i] = idx < 2 * Geo::HP ? hh * Geo::NP + pimg * Geo::HP + pix : -1;
+      } else {
+        const int idx = t + i * NP_T, pix = idx >> 1;
+        hi[i] = 0;
+        hy[i] = pix / Geo::HW;
+        hx[i] = pix - hy[i] * Geo::HW;
+        ldso[i] = idx < 2 * Geo::NP ? hh * Geo::NP + pix : -1;
+      }
     }
   }
 
@@ -200,8 +210,8 @@ struct XProducer {
     r1 = mkrsrc(p.in1 ? p.in1 + (size_t)t.n0 * img * p.c1 : p.in0);
     const int ctot = p.c0 + p.c1;
     // act == ACT_NONE: the coefficient loads still issue (fixed vmcnt arithmetic) from the input
-    ra = p.actA ? mkrsrc(p.actA + (size_t)t.n0 * ctot) : r0;
-    rb = p.actB ? mkrsrc(p.actB + (size_t)t.n0 * ctot) : r0;
+    ra = p.actA ? mkrsrc(p.actA + ((size_t)t.n0 + pimg) * ctot) : r0;
+    rb = p.actB ? mkrsrc(p.actB + ((size_t)t.n0 + pimg) * ctot) : r0;
     tn0 = t.n0;
     if (SKIP) {
 #pragma unroll

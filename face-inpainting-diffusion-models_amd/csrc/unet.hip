@@ -607,8 +607,15 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   // 3xf16 1x1 conv (attention qkv / proj_out): the split kernel's 1x1 chunks over the raw operand,
   // act(GN(x)) materialised first when the conv has a prologue (act_apply, the conv prologue's
   // fp32 arithmetic)
+  // development switches (bisecting): IFD_X3_OFF=mask: 1 no 16x16 tiles, 2 no split-K, 4 no skip layers,
+  // 8 no 8x8 four-image tiles, 16 no 1x1-only launches
+  static const int x3_off = getenv("IFD_X3_OFF") ? atoi(getenv("IFD_X3_OFF")) : 0;
+  auto x3_masked_for = [&](const ConvParams& g) {
+    return ((x3_off & 1) && g.TW == 16) || ((x3_off & 2) && g.ksplit > 1) || ((x3_off & 4) && cw.has_skip) ||
+           ((x3_off & 8) && g.TW == 8) || ((x3_off & 16) && cw.taps == 1);
+  };
   if (prec_ == IFD_PREC_3XF16 && cw.taps == 1 && cw.x3_ok && cw.x3s_off && epi == EPI_NHWC && !in1 &&
-      xf == XF_NONE) {
+      xf == XF_NONE && !x3_masked_for(p)) {
     ConvParams q = p;
     q.in0 = nullptr; q.c0 = 0; q.in1 = nullptr; q.c1 = 0; q.cin_pad = 0; q.act = ACT_NONE;
     q.s0 = act != ACT_NONE ? ws_ + o_pool_ : in0; q.sc0 = c0; q.s1 = nullptr; q.sc1 = 0;
@@ -666,10 +673,9 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
       }
     }
   }
-  // development switches (bisecting): IFD_X3_OFF=mask: 1 no 16x16 tiles, 2 no split-K, 4 no skip layers
-  static const int x3_off = getenv("IFD_X3_OFF") ? atoi(getenv("IFD_X3_OFF")) : 0;
-  const bool x3_masked = ((x3_off & 1) && p.TW == 16) || ((x3_off & 2) && p.ksplit > 1) || ((x3_off & 4) && cw.has_skip);
+  const bool x3_masked = x3_masked_for(p);
   const bool use_x3 = prec_ == IFD_PREC_3XF16 && cw.x3_ok && !x3_masked && conv_x3_eligible(p, cw.taps, xf, cw.bn);
+  IFD_REQUIRE(use_x3 || p.cin_pad == cw.cin_pad, "1x1-only operand rewrite without the split kernel");
   if (use_x3) {
     p.wpack = wblob_ + cw.x3_off;
     if (cw.has_skip) p.wskip = wblob_ + cw.x3s_off;

@@ -95,6 +95,30 @@ def test_x3_matches_fp32_batch(x3_model):
     assert maxabs(y1, y3[1:2]) <= 2e-5
 
 
+def test_x3_matches_fp32_batch4(x3_model):
+    """B=4: the batch sizes that are a multiple of 4 run the 8x8 layers as tiles of four whole
+    images and the attention 1x1s as split-kernel launches; against the fp32 mode, and each image
+    against its own B=1 run (the four images of a tile stay independent)."""
+    from ifd.model import DiffusionInpaintingModel
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(4, 3, 256, 256, device=DEV, generator=g)
+    gt = torch.rand(4, 3, 256, 256, device=DEV, generator=g) * 2 - 1
+    mask = (torch.rand(4, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
+    t = torch.tensor([999, 640, 120, 7], device=DEV)
+    m32 = DiffusionInpaintingModel(FULL, device=DEV)
+    m32.load_state_dict(make_state_dict(FULL, seed=1))
+    with torch.no_grad():
+        y3, ks = _kernels_run(x3_model, lambda: x3_model(x, t, masked_image=gt * (1 - mask), mask=mask))
+        y32 = m32(x, t, masked_image=gt * (1 - mask), mask=mask)
+        y1 = x3_model(x[2:3], t[2:3], masked_image=(gt * (1 - mask))[2:3], mask=mask[2:3])
+    assert any(k.startswith("conv_x3_kernel") and k.endswith(",8>") for k in ks), sorted(ks)
+    assert torch.isfinite(y3).all()
+    err = maxabs(y3, y32)
+    print(f"3xf16 vs fp32 B=4 maxabs={err:.3g}")
+    assert err <= 2e-5
+    assert maxabs(y1, y3[2:3]) <= 2e-5
+
+
 @pytest.mark.parametrize("name", ["c1_full_cos10_eta0.9", "c1_full_cos10_eta0"])
 def test_x3_script_ddim_full_c1(loops, meta, x3_model, name):
     """C1 loops under the split mode, held to the same oracle-envelope bound as the fp32 mode
