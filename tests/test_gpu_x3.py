@@ -119,6 +119,25 @@ def test_x3_matches_fp32_batch4(x3_model):
     assert maxabs(y1, y3[2:3]) <= 2e-5
 
 
+def test_x3_matches_fp32_bench_batch(x3_model):
+    """The bench configuration itself (B=16 at 256x256, the geometry bench.py times: blk_major
+    units, four-image 8x8 tiles, split-K 1x1 launches): 3xf16 against fp32 at two timesteps."""
+    from ifd.model import DiffusionInpaintingModel
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(16, 3, 256, 256, device=DEV, generator=g)
+    gt = torch.rand(16, 3, 256, 256, device=DEV, generator=g) * 2 - 1
+    mask = (torch.rand(16, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
+    t = torch.tensor([999] * 8 + [250] * 8, device=DEV)
+    m32 = DiffusionInpaintingModel(FULL, device=DEV)
+    m32.load_state_dict(make_state_dict(FULL, seed=1))
+    with torch.no_grad():
+        y3 = x3_model(x, t, masked_image=gt * (1 - mask), mask=mask)
+        y32 = m32(x, t, masked_image=gt * (1 - mask), mask=mask)
+    err = maxabs(y3, y32)
+    print(f"3xf16 vs fp32 B=16 maxabs={err:.3g}")
+    assert torch.isfinite(y3).all() and err <= 2e-5
+
+
 @pytest.mark.parametrize("name", ["c1_full_cos10_eta0.9", "c1_full_cos10_eta0"])
 def test_x3_script_ddim_full_c1(loops, meta, x3_model, name):
     """C1 loops under the split mode, held to the same oracle-envelope bound as the fp32 mode
