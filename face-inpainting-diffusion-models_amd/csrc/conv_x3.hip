@@ -61,6 +61,25 @@ namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) f16x8 lds_h8;
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u4;
+
+// The f16 split of two values: hi = f16(v) (one v_cvt_pk_f16_f32 for the pair), lo = f16(v - hi)
+// by v_fma_mix{lo,hi}_f16 reading hi's halves as f16 (v - hi is exact in fp32, rounded once). The
+// empty asm pins v as an fp32 register value: the compiler would otherwise fold the product that
+// makes v into a v_fma_mix conversion — a single rounding for one use of hi and a double one for
+// the other.
+__device__ __forceinline__ void split2(float v0, float v1, unsigned& h, unsigned& l) {
+  asm volatile("" : "+v"(v0), "+v"(v1));
+  const f16x2 h2 = __builtin_convertvector(f32x2{v0, v1}, f16x2);
+  h = __builtin_bit_cast(unsigned, h2);
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(l)
+      : "v"(v0), "v"(v1), "v"(h));
+}
+
 
 constexpr int XBN = 64;
 constexpr int XNPMAX = 400;                    // halo pixels of the largest tile (4 images x 10 x 10)
@@ -149,6 +168,10 @@ __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int
   t.n0 = (bx >> d.lty) << d.limg;
   return t;
 }
+
+#ifndef X3_PINF
+#define X3_PINF 1
+#endif
 
 template <int ITEMS>
 struct XSet {
@@ -322,23 +345,41 @@ struct XProducer {
     return t * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(t * -1.4426950408889634f));
   }
 
-  // prologue + split: hi plane at slot ldso, lo plane 2 planes further
+  // prologue + split: hi plane at slot ldso, lo plane 2 planes further. The activation kind is
+  // uniform: one branch per store, not two v_cndmask per value (13 % of the producer's VALU).
   __device__ __forceinline__ void store(const Set& s, int act, lds_f* As) const {
+    if (act == ACT_AFFINE_SILU)
+      store_act<ACT_AFFINE_SILU>(s, As);
+    else if (act == ACT_NONE)
+      store_act<ACT_NONE>(s, As);
+    else
+      store_act<ACT_AFFINE>(s, As);
+  }
+  template <int ACT>
+  __device__ __forceinline__ void store_act(const Set& s, lds_f* As) const {
     if (X3_ABLATE == 1 || X3_ABLATE == 2 || X3_ABLATE >= 8) return;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       if (ldso[i] >= 0) {
-        f16x8 h8, l8;
+        // SiLU: the zero padding rides in the exponent — 2^(+inf) = inf, rcp(1 + inf) = 0, t * 0 = 0
+        // for the finite t of a padding pixel — instead of a multiply by the validity per value
+        const float pinf = s.vld[i] != 0.f ? 0.f : __builtin_inff();
+        float v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int g = j >> 2, c = j & 3;
-          const float v = act1(s.raw[i][g][c], s.ca[g][c], s.cb[g][c], act) * s.vld[i];
-          const _Float16 hv = (_Float16)v;
-          h8[j] = hv;
-          l8[j] = (_Float16)(v - (float)hv);  // exact difference, rounded once
+          if (ACT == ACT_AFFINE_SILU && X3_PINF) {
+            const float t = fmaf(s.ca[g][c], s.raw[i][g][c], s.cb[g][c]);
+            v[j] = t * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(fmaf(t, -1.4426950408889634f, pinf)));
+          } else {
+            v[j] = act1(s.raw[i][g][c], s.ca[g][c], s.cb[g][c], ACT) * s.vld[i];
+          }
         }
-        *(lds_h8*)(As + 4 * ldso[i]) = h8;
-        *(lds_h8*)(As + 4 * (ldso[i] + 2 * Geo::NP)) = l8;
+        unsigned h[4], l[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) split2(v[2 * k], v[2 * k + 1], h[k], l[k]);
+        *(lds_u4*)(As + 4 * ldso[i]) = u32x4{h[0], h[1], h[2], h[3]};
+        *(lds_u4*)(As + 4 * (ldso[i] + 2 * Geo::NP)) = u32x4{l[0], l[1], l[2], l[3]};
       }
     }
   }
