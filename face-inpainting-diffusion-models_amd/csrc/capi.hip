@@ -177,4 +177,23 @@ int ifd_blend(const float* result, const float* gt, const float* mask, int64_t B
   return 0;
 }
 
+int ifd_to_u8(const float* sample, int64_t B, int C, int H, int W, uint8_t* out_nhwc, void* stream) {
+  if (B < 0 || C <= 0 || H <= 0 || W <= 0 || B * H * W > INT32_MAX) { set_error("ifd_to_u8: bad shape"); return 2; }
+  if (B == 0) return 0;  /* an empty tensor may carry a null pointer */
+  if (!sample || !out_nhwc) { set_error("ifd_to_u8: null argument"); return 2; }
+  ifd::launch_to_u8(sample, out_nhwc, (int)B, C, H * W, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return 1; }
+  return 0;
+}
+
+int ifd_mask_from_gray(const uint8_t* gray, int64_t n, float* mask, void* stream) {
+  if (n < 0 || ((!gray || !mask) && n > 0)) { set_error("ifd_mask_from_gray: bad argument"); return 2; }
+  if (n == 0) return 0;
+  ifd::launch_mask_from_gray(gray, mask, n, (hipStream_t)stream);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return 1; }
+  return 0;
+}
+
 }  // extern "C"

@@ -32,5 +32,7 @@ int launch_act_pool(const float* x, int C, int N, int Hin, int act, const float*
                     float* out_raw, hipStream_t s);
 void launch_blend(const float* res, const float* gt, const float* mask, float* out, int N, int C, int HW,
                   hipStream_t s);
+void launch_to_u8(const float* x, unsigned char* out, int N, int C, int HW, hipStream_t s);
+void launch_mask_from_gray(const unsigned char* g, float* m, int64_t n, hipStream_t s);
 
 }  // namespace ifd

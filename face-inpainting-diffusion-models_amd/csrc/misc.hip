@@ -387,6 +387,40 @@ void launch_blend(const float* res, const float* gt, const float* mask, float* o
   hipLaunchKernelGGL(blend_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, res, gt, mask, out, N, C, HW);
 }
 
+// toU8 (code/test_inp_ddim_50.py:33-41): NCHW fp32 in [-1,1] -> NHWC u8,
+// ((x + 1) * 127.5).clamp(0, 255) then a truncating cast. One thread per pixel: channel reads are
+// coalesced across the wave (stride HW), the C output bytes of a pixel are contiguous.
+__global__ void to_u8_kernel(const float* __restrict__ x, unsigned char* __restrict__ out, int N, int C, int HW) {
+#pragma clang fp contract(off)
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * HW) return;
+  const int px = idx % HW, n = idx / HW;
+  const float* src = x + (size_t)n * C * HW + px;
+  unsigned char* dst = out + (size_t)idx * C;
+  for (int c = 0; c < C; ++c) {
+    float v = (src[(size_t)c * HW] + 1.0f) * 127.5f;
+    v = fminf(fmaxf(v, 0.0f), 255.0f);
+    dst[c] = (unsigned char)(int)v;
+  }
+}
+
+void launch_to_u8(const float* x, unsigned char* out, int N, int C, int HW, hipStream_t s) {
+  const int tot = N * HW;
+  hipLaunchKernelGGL(to_u8_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, x, out, N, C, HW);
+}
+
+// OrderedMaskDataset mask convention (code/data/dataset.py:278-286): ToTensor's gray/255 in fp32,
+// then (m < 0.5).float() -> 1 = hole (black), 0 = keep (white).
+__global__ void mask_from_gray_kernel(const unsigned char* __restrict__ g, float* __restrict__ m, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  m[i] = ((float)g[i] / 255.0f < 0.5f) ? 1.0f : 0.0f;
+}
+
+void launch_mask_from_gray(const unsigned char* g, float* m, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(mask_from_gray_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g, m, n);
+}
+
 // act + 2x2 average pool, 4 channels per thread (16-byte loads/stores, coalesced along C).
 __global__ __launch_bounds__(256) void act_pool_kernel(const float* __restrict__ x, int C, int N, int Hin, int act,
                                                        const float* __restrict__ A, const float* __restrict__ B,

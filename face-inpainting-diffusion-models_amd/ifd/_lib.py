@@ -69,6 +69,9 @@ EXPORTS = {
                         + [ctypes.c_void_p] * 5 + [ctypes.POINTER(StepCoeffs), ctypes.c_void_p]),
     "ifd_blend": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "ifd_to_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_void_p, ctypes.c_void_p]),
+    "ifd_mask_from_gray": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 # conv arithmetic modes (include/ifd.h IFD_PREC_*)

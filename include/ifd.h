@@ -100,6 +100,12 @@ int ifd_ddpm_update(const float* out6, int64_t B, int H, int W, float* img, cons
                     const float* noise, const float* known, const ifd_step_coeffs* c, void* stream);
 int ifd_blend(const float* result, const float* gt, const float* mask, int64_t B, int C, int H, int W, float* out,
               void* stream);
+/* Output conversion toU8 (code/test_inp_ddim_50.py:33-41): sample NCHW fp32 -> out NHWC u8
+ * [B,H,W,C], ((x + 1) * 127.5).clamp(0, 255) with a truncating cast. B == 0 is a no-op. */
+int ifd_to_u8(const float* sample, int64_t B, int C, int H, int W, uint8_t* out_nhwc, void* stream);
+/* Mask convention of OrderedMaskDataset (code/data/dataset.py:278-286): gray u8 (already resized)
+ * -> mask fp32, 1 where gray/255 < 0.5 (black = hole), else 0. n elements, n == 0 is a no-op. */
+int ifd_mask_from_gray(const uint8_t* gray, int64_t n, float* mask, void* stream);
 
 /* Per-launch profiler: when enabled, every kernel the handle launches is bracketed by hipEvents on
  * its stream; after the caller synchronises, ifd_profile_report writes a JSON summary per kernel

@@ -1,0 +1,59 @@
+"""Output conversion and mask convention on the HIP library, bit-exact against the reference's torch
+arithmetic: toU8 (code/test_inp_ddim_50.py:33-41) and OrderedMaskDataset's mask rule
+(code/data/dataset.py:278-289: ToTensor's gray/255, then (m < 0.5).float()). Edge cases: values at
+and beyond +-1, the 127/128 gray boundary, empty batches, ragged sizes."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def ref_to_u8(sample):
+    # code/test_inp_ddim_50.py:37-40
+    s = ((sample + 1) * 127.5).clamp(0, 255).to(torch.uint8)
+    return s.permute(0, 2, 3, 1).contiguous().numpy()
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 256, 256), (3, 3, 17, 29), (2, 1, 5, 7), (16, 3, 64, 64)])
+def test_to_u8_bitexact(shape):
+    from ifd.data import toU8
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.rand(shape, generator=g) * 2.4 - 1.2  # includes out-of-range values on both sides
+    flat = x.view(-1)
+    edges = torch.tensor([-1.0, 1.0, 0.0, -1.5, 1.5, 1 / 127.5 - 1, 0.999999, -0.999999])
+    flat[: edges.numel()] = edges[: flat.numel()]
+    got = toU8(x.to(DEV))
+    want = ref_to_u8(x)
+    assert got.dtype == np.uint8 and got.shape == want.shape
+    assert np.array_equal(got, want)
+
+
+def test_to_u8_empty_and_none():
+    from ifd.data import toU8
+    assert toU8(None) is None
+    out = toU8(torch.zeros(0, 3, 8, 8, device=DEV))
+    assert out.shape == (0, 8, 8, 3)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 256, 256), (4, 1, 33, 31), (0, 1, 4, 4)])
+def test_mask_from_gray_bitexact(shape):
+    from ifd.data import mask_from_gray
+    g = torch.Generator().manual_seed(3)
+    gray = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8)
+    if gray.numel() >= 256:
+        gray.view(-1)[:256] = torch.arange(256, dtype=torch.uint8)  # every gray level incl. 127/128
+    want = ((gray.float() / 255) < 0.5).float()  # ToTensor (div 255 in fp32), dataset.py:286
+    got = mask_from_gray(gray.to(DEV)).cpu()
+    assert torch.equal(got, want)
+    if gray.numel() >= 256:
+        assert got.view(-1)[127] == 1 and got.view(-1)[128] == 0
+
+
+def test_data_rejects_cpu_tensors():
+    from ifd.data import mask_from_gray, to_u8_device
+    with pytest.raises(RuntimeError):
+        to_u8_device(torch.zeros(1, 3, 4, 4))
+    with pytest.raises(RuntimeError):
+        mask_from_gray(torch.zeros(1, 1, 4, 4, dtype=torch.uint8))
