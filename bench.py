@@ -6,9 +6,13 @@ synthetic 256x256 inputs, per GPU. Workload = BASELINE.json configs[1]: batch 16
 cosine T=1000, eta 0.75 (code/test_inp_ddim_100.py:820), fp32, random-init weights of the
 reference architecture (seeded manifest), gt ~ U(-1,1), 25 % centre-square + random-rectangle masks.
 N GPUs = N independent shards (weak scaling), one RCCL all_gather of the outputs inside the
-timed region.
+timed region. `--gpus N` without a torch.distributed.run environment starts N ranks itself (a
+torch.distributed.run child launched before this process touches the GPU) and relays rank 0's
+line. `--noise parity` draws every noise tensor for the whole global batch on the host in the
+reference's order and keeps the rank's rows (SURVEY §8e: results independent of the GPU count);
+the default `device` mode draws per rank on the GPU (the throughput configuration).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--noise device|parity]
 """
 from __future__ import annotations
 
@@ -84,6 +88,27 @@ def cpu_baseline(budget_s, H=256):
             "s_per_unet_eval": t_eval, "cpu_model": cpu_model}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """Run this script as N ranks under torch.distributed.run (one process per GPU) and return its
+    exit code. Called before anything here touches the GPU; the child is a separate process (no
+    exec), and its stdout (rank 0's JSON line) is inherited."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,7 +123,12 @@ def main():
                     help="conv arithmetic: the fp32-accurate 3xf16 split MFMA (default), or exact fp32 MFMA")
     ap.add_argument("--fp32-exact-steps", type=int, default=1,
                     help="N=1 only: also time this many steps in exact-fp32 mode (0 = skip)")
+    ap.add_argument("--noise", choices=["device", "parity"], default="device",
+                    help="device: per-rank GPU RNG (throughput); parity: full-batch host draws in reference order, "
+                         "sliced per rank (GPU-count-independent results)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     from ifd import parallel
     from ifd.manifest import make_state_dict
@@ -109,7 +139,9 @@ def main():
     from ifd import _lib
 
     rank, ws, local = parallel.world()
-    dev = torch.device("cuda", local)
+    if ws != args.gpus and rank == 0:
+        print(f"bench: WORLD_SIZE={ws} overrides --gpus {args.gpus}", file=sys.stderr)
+    dev = parallel.device_for(local)
     torch.cuda.set_device(dev)
     parallel.init(device=dev)
     B, H = args.batch, FULL.image_size
@@ -118,15 +150,21 @@ def main():
     model.load_state_dict(make_state_dict(FULL, seed=1))
     model.eval()
     diffusion = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="cosine")
-    sampler = InpaintingSampler(model, diffusion, ddim_timesteps=args.ddim_steps, device=dev)
-    gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
+    if args.noise == "parity":
+        lo, hi = parallel.shard_range(B * ws, rank, ws)
+        sampler = InpaintingSampler(model, diffusion, ddim_timesteps=args.ddim_steps, device=dev, noise_device="cpu",
+                                    noise_shard=(lo, hi, B * ws))
+        gt, mask = (v[lo:hi].contiguous() for v in synth_inputs(B * ws, H, seed=7, device=dev))
+    else:
+        sampler = InpaintingSampler(model, diffusion, ddim_timesteps=args.ddim_steps, device=dev)
+        gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
     shape = (B, 3, H, H)
     n_evals = len(sampler.create_ddim_timestep_sequence(1000, args.ddim_steps))
     handle = model.handle(dev)
     L = _lib.lib()
 
     def one_pass(i):
-        torch.manual_seed(42 + 1000 * rank + i)
+        torch.manual_seed(42 + i if args.noise == "parity" else 42 + 1000 * rank + i)
         with torch.no_grad():
             y = sampler.inpainting_ddim_sample_loop(sampler.model_fn, shape, gt, mask, True, dev, False, args.eta)
             y = sampler.final_blend(y, gt, mask)
@@ -211,6 +249,7 @@ def main():
                                "accumulator; error vs an fp64 UNet equals fp32's (tests/test_cpu_split_numerics.py) "
                                "and every GPU parity test holds at the fp32 tolerances (tests/test_gpu_x3.py)")},
         "data": "synthetic (gt~U(-1,1), centre-square + rectangle masks, seeded random-init weights)",
+        "noise": args.noise,
         "config": {"workload": "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1])",
                    "global_batch": B * ws, "batch_per_gpu": B, "unet_evals_per_image": n_evals,
                    "gflop_per_unet_eval_per_image": round(gflop_per_image(FULL), 2),

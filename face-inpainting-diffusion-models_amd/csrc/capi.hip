@@ -88,6 +88,26 @@ int ifd_get_precision(ifd_handle* h, int* prec) {
   return 0;
 }
 
+int ifd_guard_reset(ifd_handle* h, void* stream) {
+  if (!h) { set_error("null handle"); return 2; }
+  return h->model->guard_reset((hipStream_t)stream);
+}
+
+int ifd_guard_read(ifd_handle* h, int* tripped, void* stream) {
+  if (!h || !tripped) { set_error("ifd_guard_read: null argument"); return 2; }
+  return h->model->guard_read((hipStream_t)stream, tripped);
+}
+
+int ifd_set_option(ifd_handle* h, const char* key, int value) {
+  if (!h || !key) { set_error("ifd_set_option: null argument"); return 2; }
+  return h->model->set_option(key, value);
+}
+
+int ifd_get_option(ifd_handle* h, const char* key, int* value) {
+  if (!h || !key || !value) { set_error("ifd_get_option: null argument"); return 2; }
+  return h->model->get_option(key, value);
+}
+
 int ifd_memory(ifd_handle* h, int64_t* wb, int64_t* ws) {
   if (!h) { set_error("null handle"); return 2; }
   if (wb) *wb = h->model->weight_bytes();

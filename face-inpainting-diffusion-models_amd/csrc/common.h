@@ -30,6 +30,34 @@ const char* get_error();
     }                                                                                    \
   } while (0)
 
+// Launchers keep one-time per-device state (large-LDS attribute set, CU count). One process may
+// drive several devices through several handles, so the state is keyed by the device ordinal.
+constexpr int kMaxDevices = 64;
+inline int current_device() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return (d >= 0 && d < kMaxDevices) ? d : 0;
+}
+inline int device_cu_count() {
+  static int ncu[kMaxDevices] = {};
+  const int d = current_device();
+  if (!ncu[d]) {
+    int n = 0;
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
+    ncu[d] = n > 0 ? n : 256;
+  }
+  return ncu[d];
+}
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device); `done` is the
+// caller's per-kernel table.
+inline hipError_t set_lds_attr_once(bool (&done)[kMaxDevices], const void* fn, int bytes) {
+  const int d = current_device();
+  if (done[d]) return hipSuccess;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done[d] = true;
+  return e;
+}
+
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
 }  // namespace ifd

@@ -80,6 +80,13 @@ struct ConvParams {
   // Written only for single-image tiles without split-K (the host checks).
   float* gstat;
   int gstat_E;
+  // handle options (read once at ifd_create, ifd_set_option): development overrides and the
+  // batch-invariant geometry (split-K and tile kind chosen per image, not per batch, so an image's
+  // result does not depend on how many other images share the launch)
+  int opt_bm128, opt_lds_pad, opt_stream_cw, opt_invariant;
+  // 3xf16 range guard (conv_x3.hip): set to 1 when an operand's magnitude reaches the f16 range
+  // (|a| >= 65504 would split into inf). The host re-runs the eval in fp32 when it is set.
+  unsigned* guard;
 };
 
 // Launch with the tile configuration chosen from (cout, taps, xform). Returns hipError_t.

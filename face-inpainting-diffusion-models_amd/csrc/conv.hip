@@ -534,8 +534,7 @@ static int launch_one(const ConvParams& p, hipStream_t stream) {
   const int npA = NP > BM ? NP : BM;
   const size_t stage = (size_t)(2 * npA * 8 + 2 * 9 * 8 * BN);
   const size_t epi = (size_t)BM * (BN + 4);  // NHWC epilogue tile (the final-conv tile is smaller)
-  static const char* pad_env = getenv("IFD_CONV_LDS_PAD");  // development: force 1 block / CU
-  const size_t pad = pad_env ? (size_t)atoi(pad_env) : 0;
+  const size_t pad = (size_t)p.opt_lds_pad;  // development option: force 1 block / CU
   const size_t lds = (stage > epi ? stage : epi) * sizeof(float) + pad;
   const bool one = p.IMGS == 1;
   if constexpr (BM == 256) {  // only used for W >= 32 (one image per tile, 2*NP <= 1024)
@@ -561,16 +560,15 @@ int conv_pick_bn(int cout, int taps, int H, int W, int N) {
 // the grid still gives >= 2 blocks per CU: it halves the weight-slab loads per MFMA, the producer's
 // bottleneck. Otherwise BM = 128, with split-K to cover the chip on the low-resolution layers.
 void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool x3) {
-  static const char* ov = getenv("IFD_CONV_BM");  // development override: 128 disables BM=256
-  const bool allow256 = !(ov && atoi(ov) == 128);
+  const bool allow256 = !p.opt_bm128;  // development option: 128-pixel tiles only
   int bm = 128;
   if (x3) {
     // 3xf16 split kernel (conv_x3.hip): 256-pixel tiles of one image (8 x 32 or 16 x 16) whatever
     // the tile count (persistent grid); nchunks = 16-channel chunks of the whole K stream
     if (bn == 64 && W >= 16 && H >= 256 / (W < 32 ? W : 32)) bm = 256;
-    if (bn == 64 && W == 8 && H == 8 && N % 4 == 0) bm = 256;  // four whole 8 x 8 images per tile
+    if (bn == 64 && W == 8 && H == 8 && N % 4 == 0 && !p.opt_invariant) bm = 256;  // four whole 8 x 8 images per tile
   } else if (allow256 && bn == 64 && W >= 32 && H >= 8) {
-    const long blocks256 = (long)N * (H / 8) * (W / 32) * (p.cout_pad / bn);
+    const long blocks256 = (long)(p.opt_invariant ? 1 : N) * (H / 8) * (W / 32) * (p.cout_pad / bn);
     if (blocks256 >= 512) bm = 256;
   }
   p.bm = bm;
@@ -583,7 +581,8 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
   p.lg_tpi = __builtin_ctz(p.TH * p.TW);
   const int tiles_n = (N + p.IMGS - 1) / p.IMGS;
   p.npix_tiles = tiles_n * p.tiles_y * p.tiles_x;
-  const long blocks = (long)p.npix_tiles * (p.cout_pad / bn);
+  // batch-invariant option: split as if the launch held one image (tile row) only
+  const long blocks = (long)(p.opt_invariant ? (p.npix_tiles / tiles_n) : p.npix_tiles) * (p.cout_pad / bn);
   int S = 1;
   if (x3 && bm == 256) {
     // persistent units: split K until the units cover the 256 CUs, keeping >= 4 chunks per unit

@@ -597,20 +597,10 @@ bool conv_stream_eligible(const ConvParams& p, int taps, int xform, int bn) {
 
 template <int XF, int CW>
 static int launch_stream_inst(const ConvParams& p, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_stream_kernel<XF, CW>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  static bool attr_set[kMaxDevices] = {};
+  hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_stream_kernel<XF, CW>), 160 * 1024);
+  if (e != hipSuccess) return (int)e;
+  const int ncu = device_cu_count();
   const int nvirt = p.npix_tiles * (p.cout_pad / SBN);
   const int grid = nvirt < ncu ? nvirt : ncu;  // one workgroup per CU (LDS-bound)
   hipLaunchKernelGGL((conv_stream_kernel<XF, CW>), dim3(grid), dim3(64 * CW + NP_T), conv_stream_lds_bytes(), stream, p);
@@ -619,21 +609,11 @@ static int launch_stream_inst(const ConvParams& p, hipStream_t stream) {
 
 template <int XF>
 static int launch_stream2_inst(const ConvParams& p, hipStream_t stream) {
-  static bool attr_set = false;
+  static bool attr_set[kMaxDevices] = {};
   const size_t lds = (size_t)S2_LDS_FLOATS * sizeof(float);
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_stream2_kernel<XF>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_stream2_kernel<XF>), (int)lds);
+  if (e != hipSuccess) return (int)e;
+  const int ncu = device_cu_count();
   const int nvirt = p.npix_tiles * (p.cout_pad / SBN);
   const int grid = nvirt < 2 * ncu ? nvirt : 2 * ncu;  // two workgroups per CU
   hipLaunchKernelGGL((conv_stream2_kernel<XF>), dim3(grid), dim3(NT), lds, stream, p);
@@ -646,8 +626,7 @@ int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t str
     if (xform == XF_UP) return launch_stream2_inst<XF_UP>(p, stream);
     return (int)hipErrorInvalidValue;
   }
-  const char* cw_env = getenv("IFD_STREAM_CW");  // development: 4 or 8 consumer waves
-  const bool cw4 = cw_env && atoi(cw_env) == 4;
+  const bool cw4 = p.opt_stream_cw == 4;  // development option: 4 or 8 consumer waves
   if (xform == XF_NONE) return cw4 ? launch_stream_inst<XF_NONE, 4>(p, stream) : launch_stream_inst<XF_NONE, 8>(p, stream);
   if (xform == XF_UP) return cw4 ? launch_stream_inst<XF_UP, 4>(p, stream) : launch_stream_inst<XF_UP, 8>(p, stream);
   return (int)hipErrorInvalidValue;  // avg-pool prologue: conv.hip (its 4-source register sets do not fit 3 deep)

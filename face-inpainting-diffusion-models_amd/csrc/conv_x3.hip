@@ -203,6 +203,7 @@ struct XProducer {
                // strided buffer view (stride = the source's channel count x 4 B)
   int skq;     // byte offset of this lane's swizzled channel quad (see dma)
   float valid[IT];
+  float gmax = 0.f;  // range guard: largest |operand| this thread split
 
   __device__ __forceinline__ void init(int t) {
     ptid = t;
@@ -347,7 +348,7 @@ struct XProducer {
 
   // prologue + split: hi plane at slot ldso, lo plane 2 planes further. The activation kind is
   // uniform: one branch per store, not two v_cndmask per value (13 % of the producer's VALU).
-  __device__ __forceinline__ void store(const Set& s, int act, lds_f* As) const {
+  __device__ __forceinline__ void store(const Set& s, int act, lds_f* As) {
     if (act == ACT_AFFINE_SILU)
       store_act<ACT_AFFINE_SILU>(s, As);
     else if (act == ACT_NONE)
@@ -356,7 +357,7 @@ struct XProducer {
       store_act<ACT_AFFINE>(s, As);
   }
   template <int ACT>
-  __device__ __forceinline__ void store_act(const Set& s, lds_f* As) const {
+  __device__ __forceinline__ void store_act(const Set& s, lds_f* As) {
     if (X3_ABLATE == 1 || X3_ABLATE == 2 || X3_ABLATE >= 8) return;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -375,6 +376,9 @@ struct XProducer {
             v[j] = act1(s.raw[i][g][c], s.ca[g][c], s.cb[g][c], ACT) * s.vld[i];
           }
         }
+        // range guard: |v| >= 65504 would split into an f16 inf (max3 chains: ~0.6 VALU op per value)
+        gmax = fmaxf(gmax, fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
+                                 fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
         unsigned h[4], l[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) split2(v[2 * k], v[2 * k + 1], h[k], l[k]);
@@ -442,7 +446,7 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
 // split in registers with the producers' arithmetic (a_hi = f16(a), a_lo = f16(a - a_hi)), then
 // the 3 split products x 2 x 2 fragment blocks. pb = tile pixel.
 __device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws,
-                                             const int (&pb)[2]) {
+                                             const int (&pb)[2], float& gmax) {
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const lds_f* Wb = Ws + 4 * (h * XBN + l32);
   f16x8 ah[2], al[2], bs[2], bl[2];
@@ -454,6 +458,7 @@ __device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* A
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float v = j < 4 ? q0[j] : q1[j - 4];
+      gmax = fmaxf(gmax, fabsf(v));  // range guard (the raw residual stream is not normalised)
       const _Float16 hv = (_Float16)v;
       ah[mr][j] = hv;
       al[mr][j] = (_Float16)(v - (float)hv);
@@ -640,6 +645,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     };
     zero();
     XBARRIER_CONSUMER();  // chunk 0 staged
+    float gmax = 0.f;
     int kk = 0, u = 0, z = 0;
     STile t = unit_of(0, z);
     for (int j = 0; j < J; ++j) {
@@ -652,7 +658,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       } else if (!SKIP || c < nmain) {
         consume_x3<TW>(acc, A0 + (j & 1) * XA, Ws, pb);
       } else {
-        consume_skip(acc, Ws + XSKA, Ws, pbs);
+        consume_skip(acc, Ws + XSKA, Ws, pbs, gmax);
       }
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
         p.trace[64 * blockIdx.x + 16 + j] = __builtin_amdgcn_s_memtime();
@@ -667,6 +673,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       }
       if (X3_ABLATE != 10) XBARRIER_CONSUMER();
     }
+    if (SKIP && p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
     return;
   }
 
@@ -751,25 +758,16 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     stamp(32, j + 1);
     barrier();
   }
+  if (p.guard && P.gmax >= 65504.0f) atomicOr(p.guard, 1u);
 }
 
 template <int XF, bool SKIP, int TW>
 static int launch_x3_inst(const ConvParams& p, hipStream_t stream) {
-  static bool attr_set = false;
+  static bool attr_set[kMaxDevices] = {};
   const size_t lds = (size_t)X_LDS_FLOATS * sizeof(float);
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<XF, SKIP, TW>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_x3_kernel<XF, SKIP, TW>), (int)lds);
+  if (e != hipSuccess) return (int)e;
+  const int ncu = device_cu_count();
   const int nunit = p.npix_tiles * (p.cout_pad / XBN) * p.ksplit;
   const int grid = nunit < ncu ? nunit : ncu;  // one workgroup per CU (LDS-bound)
   hipLaunchKernelGGL((conv_x3_kernel<XF, SKIP, TW>), dim3(grid), dim3(NT), lds, stream, p);
@@ -798,7 +796,7 @@ static int launch_x3_tw(const ConvParams& p, int xform, hipStream_t stream) {
 bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
   const int nch = p.cin_pad / 16 + (p.wskip ? p.cs_pad / 16 : 0);
   const bool one_img = (p.TW == 32 || p.TW == 16) && p.TH * p.TW == 256 && p.IMGS == 1;
-  const bool img8 = p.TW == 8 && p.TH == 8 && p.H == 8 && p.W == 8 && p.IMGS == 4 && p.N % 4 == 0 &&
+  const bool img8 = p.TW == 8 && p.TH == 8 && p.H == 8 && p.W == 8 && p.IMGS == 4 && p.N % 4 == 0 && !p.opt_invariant &&
                     xform == XF_NONE && (!p.res || p.res_xform == XF_NONE);
   const bool only1x1 = taps == 1 && p.cin_pad == 0 && p.wskip;  // a 1x1 conv: 1x1 chunks only
   return (taps == 9 || only1x1) && xform != XF_DOWN && bn == XBN && p.bm == 256 && (one_img || img8) &&

@@ -318,12 +318,8 @@ template <int KT>
 static void launch_attention_mfma(const float* qkv, int N, int C, float scale, float* out, hipStream_t s) {
   constexpr int T = 32 * KT;
   const size_t lds = (size_t)T * (AM_KS + AM_VS) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_mfma_kernel<KT>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
+  static bool attr[kMaxDevices] = {};
+  (void)set_lds_attr_once(attr, reinterpret_cast<const void*>(&attention_mfma_kernel<KT>), (int)lds);
   dim3 grid((T + 127) / 128, C / AT_CH, N);
   hipLaunchKernelGGL(attention_mfma_kernel<KT>, grid, dim3(256), lds, s, qkv, C, scale, out);
 }

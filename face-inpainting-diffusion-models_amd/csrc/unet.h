@@ -76,6 +76,11 @@ class Model {
   // Conv arithmetic: IFD_PREC_FP32 (exact fp32 MFMA) or IFD_PREC_3XF16 (split f16 MFMA, fp32-accurate)
   int set_precision(int prec);
   int precision() const { return prec_; }
+  // Handle options (ifd_set_option): initial values come from the environment once, at creation
+  // (IFD_CONV_STREAM, IFD_X3_OFF, IFD_GN_FUSED, IFD_STREAM_CW, IFD_CONV_BM, IFD_CONV_LDS_PAD,
+  // IFD_BATCH_INVARIANT); nothing is read from the environment per launch.
+  int set_option(const std::string& key, int value);
+  int get_option(const std::string& key, int* value) const;
 
  private:
   void build_plan();
@@ -149,8 +154,26 @@ class Model {
   std::map<const float*, float*> stat_area_;
   std::map<const float*, StatRec> stat_;
   bool gn_fused_ = true;
+  int opt_stream_ = 2;      // wide fp32 layers: 0 one tile per workgroup, 1/2 persistent (1 or 2 per CU)
+  int opt_x3_off_ = 0;      // bisecting mask: 1 no 16x16 tiles, 2 no split-K, 4 no skip layers, 8 no 8x8, 16 no 1x1
+  int opt_stream_cw_ = 8;   // conv_stream consumer waves (4 or 8)
+  int opt_bm128_ = 0;       // 128-pixel fp32 tiles only
+  int opt_lds_pad_ = 0;     // extra LDS bytes per fp32 conv block
+  int opt_invariant_ = 0;   // batch-invariant geometry (results independent of the batch split)
+  void fill_opts(ConvParams& p) const {
+    p.opt_bm128 = opt_bm128_;
+    p.opt_lds_pad = opt_lds_pad_;
+    p.opt_stream_cw = opt_stream_cw_;
+    p.opt_invariant = opt_invariant_;
+  }
   const float* pooled_raw_ = nullptr;  // tensor whose raw 2x2 pool sits in o_pool2_ (act_pool)
   int prec_ = 0;
+  unsigned* guard_ = nullptr;  // 3xf16 range guard word (ConvParams::guard)
+
+ public:
+  // range guard: async reset / synchronous read (0 = every split operand was in range)
+  int guard_reset(hipStream_t s);
+  int guard_read(hipStream_t s, int* tripped);
 };
 
 }  // namespace ifd

@@ -16,13 +16,63 @@
 
 namespace ifd {
 
-constexpr int kDefaultStreamMode = 2;
-
 static int ceil_to(int v, int m) { return (v + m - 1) / m * m; }
 
-Model::Model(const ifd_config& cfg) : cfg_(cfg) { build_plan(); }
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+Model::Model(const ifd_config& cfg) : cfg_(cfg) {
+  build_plan();
+  opt_stream_ = env_int("IFD_CONV_STREAM", 2);
+  opt_x3_off_ = env_int("IFD_X3_OFF", 0);
+  gn_fused_ = env_int("IFD_GN_FUSED", 1) != 0;
+  opt_stream_cw_ = env_int("IFD_STREAM_CW", 8);
+  opt_bm128_ = env_int("IFD_CONV_BM", 0) == 128;
+  opt_lds_pad_ = env_int("IFD_CONV_LDS_PAD", 0);
+  opt_invariant_ = env_int("IFD_BATCH_INVARIANT", 0) != 0;
+}
+
+int Model::set_option(const std::string& key, int v) {
+  if (key == "conv_stream") {
+    IFD_REQUIRE(v >= 0 && v <= 2, "conv_stream must be 0, 1 or 2");
+    opt_stream_ = v;
+  } else if (key == "x3_off") {
+    opt_x3_off_ = v;
+  } else if (key == "gn_fused") {
+    gn_fused_ = v != 0;
+  } else if (key == "stream_cw") {
+    IFD_REQUIRE(v == 4 || v == 8, "stream_cw must be 4 or 8");
+    opt_stream_cw_ = v;
+  } else if (key == "conv_bm128") {
+    opt_bm128_ = v != 0;
+  } else if (key == "lds_pad") {
+    IFD_REQUIRE(v >= 0 && v <= 65536, "lds_pad out of range");
+    opt_lds_pad_ = v;
+  } else if (key == "batch_invariant") {
+    if ((v != 0) != (opt_invariant_ != 0)) ws_B_ = 0;  // split-K slab sizing depends on it: re-plan
+    opt_invariant_ = v != 0;
+  } else {
+    IFD_REQUIRE(false, "unknown option " + key);
+  }
+  return 0;
+}
+
+int Model::get_option(const std::string& key, int* v) const {
+  if (key == "conv_stream") *v = opt_stream_;
+  else if (key == "x3_off") *v = opt_x3_off_;
+  else if (key == "gn_fused") *v = gn_fused_ ? 1 : 0;
+  else if (key == "stream_cw") *v = opt_stream_cw_;
+  else if (key == "conv_bm128") *v = opt_bm128_;
+  else if (key == "lds_pad") *v = opt_lds_pad_;
+  else if (key == "batch_invariant") *v = opt_invariant_;
+  else IFD_REQUIRE(false, "unknown option " + key);
+  return 0;
+}
 
 Model::~Model() {
+  if (guard_) (void)hipFree(guard_);
   if (wblob_) (void)hipFree(wblob_);
   if (ws_) (void)hipFree(ws_);
   for (auto e : ev_pool_) (void)hipEventDestroy(e);
@@ -320,6 +370,25 @@ static bool pack_conv_x3(const std::vector<float>& w, int cout, int cin, int tap
   return ok;
 }
 
+int Model::guard_reset(hipStream_t s) {
+  if (!guard_) {
+    IFD_CHECK_HIP(hipMalloc(&guard_, 64));
+    IFD_CHECK_HIP(hipMemset(guard_, 0, 64));
+  }
+  IFD_CHECK_HIP(hipMemsetAsync(guard_, 0, sizeof(unsigned), s));
+  return 0;
+}
+
+int Model::guard_read(hipStream_t s, int* tripped) {
+  *tripped = 0;
+  if (!guard_) return 0;
+  unsigned v = 0;
+  IFD_CHECK_HIP(hipMemcpyAsync(&v, guard_, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  IFD_CHECK_HIP(hipStreamSynchronize(s));
+  *tripped = v != 0;
+  return 0;
+}
+
 int Model::set_precision(int prec) {
   IFD_REQUIRE(prec == IFD_PREC_FP32 || prec == IFD_PREC_3XF16, "unknown precision mode");
   prec_ = prec;
@@ -510,6 +579,7 @@ int Model::ensure_workspace(int B) {
     for (int x3 = 0; x3 < 2; ++x3) {  // fp32 kernels' geometry and the split kernel's
       ConvParams g;
       std::memset(&g, 0, sizeof(g));
+      fill_opts(g);
       g.cout_pad = cw.cout_pad;
       const int nch = x3 ? (cw.cin_pad + (cw.has_skip ? cw.cs_pad : 0)) / 16 : cw.cin_pad / 8;
       conv_geometry(g, H, H, B, cw.bn, nch, x3 == 1);
@@ -574,6 +644,8 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                     const float* known) {
   ConvParams p;
   std::memset(&p, 0, sizeof(p));
+  fill_opts(p);
+  p.guard = guard_;
   p.in0 = in0; p.c0 = c0; p.in1 = in1; p.c1 = c1;
   p.N = N; p.Hin = Hin; p.Win = Hin; p.H = H; p.W = H;
   p.act = act; p.actA = A; p.actB = Bc;
@@ -600,16 +672,17 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   p.img = img; p.gt = gt; p.mask = mask; p.noise = noise; p.known = known;
   IFD_REQUIRE(c0 % 8 == 0 && c1 % 8 == 0 && c0 + c1 == cw.cin_pad, "conv input channels");
   IFD_REQUIRE(!cw.has_skip || (sc0 + sc1 == cw.cs_pad && sc0 % 8 == 0 && sc1 % 8 == 0), "skip channels");
-  // IFD_CONV_STREAM selects the wide-layer kernel: 0 one tile per workgroup (conv.hip), 1 one
-  // persistent workgroup per CU, 2 two persistent workgroups per CU (conv_stream.hip)
-  const char* st_env = getenv("IFD_CONV_STREAM");
-  const int stream_mode = st_env ? atoi(st_env) : kDefaultStreamMode;
+  // option conv_stream selects the wide-layer kernel: 0 one tile per workgroup (conv.hip), 1 one
+  // persistent workgroup per CU, 2 two persistent workgroups per CU (conv_stream.hip). The
+  // batch-invariant geometry keeps the one-tile kernel: the stream kernels' eligibility depends on
+  // the batch's tile count.
+  const int stream_mode = opt_invariant_ ? 0 : opt_stream_;
   // 3xf16 1x1 conv (attention qkv / proj_out): the split kernel's 1x1 chunks over the raw operand,
   // act(GN(x)) materialised first when the conv has a prologue (act_apply, the conv prologue's
   // fp32 arithmetic)
-  // development switches (bisecting): IFD_X3_OFF=mask: 1 no 16x16 tiles, 2 no split-K, 4 no skip layers,
+  // development option x3_off (bisecting): 1 no 16x16 tiles, 2 no split-K, 4 no skip layers,
   // 8 no 8x8 four-image tiles, 16 no 1x1-only launches
-  static const int x3_off = getenv("IFD_X3_OFF") ? atoi(getenv("IFD_X3_OFF")) : 0;
+  const int x3_off = opt_x3_off_;
   auto x3_masked_for = [&](const ConvParams& g) {
     return ((x3_off & 1) && g.TW == 16) || ((x3_off & 2) && g.ksplit > 1) || ((x3_off & 4) && cw.has_skip) ||
            ((x3_off & 8) && g.TW == 8) || ((x3_off & 16) && cw.taps == 1);
@@ -738,7 +811,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
       snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
     else if (use_stream)
-      snprintf(nm, sizeof(nm), "conv_stream_kernel<%d,%d>", xf, getenv("IFD_STREAM_CW") ? atoi(getenv("IFD_STREAM_CW")) : 8);
+      snprintf(nm, sizeof(nm), "conv_stream_kernel<%d,%d>", xf, opt_stream_cw_);
     else  // (BM,BN,WGM,WGN,TAPS,XF)
       snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%s,%d,%d>", p.bm, cw.bn,
                (p.bm == 256 || cw.bn == 32) ? "4,1" : "2,2", cw.taps, xf);
@@ -834,6 +907,8 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
   float* part = ws_ + o_part_;
   float* t1 = ws_ + o_t1_;
   const int H = r.xf == XF_UP ? 2 * Hin : (r.xf == XF_DOWN ? Hin / 2 : Hin);
+  // o_pool2_'s pooled residual is valid only within the block whose conv1 wrote it
+  pooled_raw_ = nullptr;
   hipEvent_t g0;
   prof_begin(s, &g0, "groupnorm_stats");
   (void)part;
@@ -884,15 +959,15 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
     if (finalize()) return 1;
   }
   if (ensure_workspace(B)) return 1;
+  if (!guard_) {
+    IFD_CHECK_HIP(hipMalloc(&guard_, 64));
+    IFD_CHECK_HIP(hipMemset(guard_, 0, 64));
+  }
   const int R = cfg_.image_size;
   const int mc = cfg_.model_channels;
   float* x0 = ws_ + o_x0_;
   stat_.clear();
   pooled_raw_ = nullptr;
-  {
-    const char* gf = getenv("IFD_GN_FUSED");  // development switch: 0 = separate statistics pass
-    gn_fused_ = !(gf && gf[0] == '0');
-  }
   hipEvent_t p0;
   prof_begin(s, &p0, "input_pack+temb+emb_proj");
   launch_pack_input(x, a, m, pack_mode, B, R * R, x0, s);

@@ -9,6 +9,10 @@ returning the [B, 6, H, W] fp32 output (eps + learned-range variance values).
 The parameters live as ordinary device tensors; on the first forward after a (re)load they are
 handed to the library (`ifd_load_weights`), which packs its own NHWC/KRSC-style copies.
 There is no CPU/PyTorch fallback: a CPU tensor or a missing library raises.
+
+precision="3xf16" is guarded: the split kernels flag any operand that reaches the f16 range
+(include/ifd.h ifd_guard_*); a flagged forward is recomputed in exact fp32 (counted in
+`guard_trips`), so the result is fp32-class for any input, not only for well-scaled weights.
 """
 from __future__ import annotations
 
@@ -75,9 +79,11 @@ class Handle:
 class DiffusionInpaintingModel(torch.nn.Module):
     """9-channel inpainting UNet (code/unet.py:176-200) executed by libifd."""
 
-    def __init__(self, cfg: UNetConfig = FULL, device=None, precision: str = "fp32"):
+    def __init__(self, cfg: UNetConfig = FULL, device=None, precision: str = "fp32", options=None):
         super().__init__()
         self.cfg = cfg
+        # handle options (include/ifd.h ifd_set_option), e.g. {"batch_invariant": 1}
+        self.options = dict(options or {})
         if precision not in _lib.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}")
         # "fp32": exact fp32 MFMA; "3xf16": split f16 MFMA with fp32-level error (include/ifd.h)
@@ -96,6 +102,7 @@ class DiffusionInpaintingModel(torch.nn.Module):
         self._handle_device = None
         self._dirty = True
         self.dtype = torch.float32
+        self.guard_trips = 0  # 3xf16 evals / loops recomputed in fp32 by the range guard
 
     # -- weights -------------------------------------------------------------------------------
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
@@ -125,7 +132,10 @@ class DiffusionInpaintingModel(torch.nn.Module):
                     del t
                 _lib.check(L.ifd_finalize(self._handle.h))
             self._dirty = False
-        _lib.check(_lib.lib().ifd_set_precision(self._handle.h, _lib.PRECISIONS[self.precision]))
+        L = _lib.lib()
+        _lib.check(L.ifd_set_precision(self._handle.h, _lib.PRECISIONS[self.precision]))
+        for k, v in self.options.items():
+            _lib.check(L.ifd_set_option(self._handle.h, k.encode(), int(v)))
         return self._handle
 
     # -- forward -------------------------------------------------------------------------------
@@ -141,18 +151,50 @@ class DiffusionInpaintingModel(torch.nn.Module):
         if not x.is_cuda:
             raise RuntimeError("ifd: the HIP UNet runs on GPU tensors only (no CPU fallback)")
         dev = x.device
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError(f"x must be [B,3,H,W], got {tuple(x.shape)}")
         B, C, H, W = x.shape
-        assert C == 3 and masked_image.shape == (B, 3, H, W) and mask.shape == (B, 1, H, W), "shape mismatch"
+        # the reference's torch.cat needs equal batch sizes; a batch-1 condition is broadcast here
+        for name, v, c in (("masked_image", masked_image, 3), ("mask", mask, 1)):
+            if not isinstance(v, torch.Tensor) or v.dim() != 4 or v.shape[1:] != (c, H, W) or v.shape[0] not in (1, B):
+                raise ValueError(f"{name} must be [{B},{c},{H},{W}], got "
+                                 f"{tuple(v.shape) if isinstance(v, torch.Tensor) else type(v)}")
         xx = self._dev_f32(x, dev, "x")
-        mi = self._dev_f32(masked_image, dev, "masked_image")
-        mk = self._dev_f32(mask, dev, "mask")
+        mi = self._dev_f32(masked_image, dev, "masked_image").expand(B, 3, H, W).contiguous()
+        mk = self._dev_f32(mask, dev, "mask").expand(B, 1, H, W).contiguous()
         tt = torch.as_tensor(t, device=dev).to(torch.int64).reshape(-1).expand(B).contiguous()
         out = torch.empty(B, self.cfg.out_channels, H, W, device=dev, dtype=torch.float32)
         h = self.handle(dev)
         L = _lib.lib()
-        _lib.check(L.ifd_unet_forward(h.h, _lib.ptr(xx), _lib.ptr(mi), _lib.ptr(mk), _lib.ptr(tt), B, H, W,
-                                      _lib.ptr(out), _lib.stream_ptr(dev)))
+        self.run_guarded(h, dev, lambda: _lib.check(L.ifd_unet_forward(
+            h.h, _lib.ptr(xx), _lib.ptr(mi), _lib.ptr(mk), _lib.ptr(tt), B, H, W, _lib.ptr(out), _lib.stream_ptr(dev))))
         return out
+
+    def run_guarded(self, h, dev, launch, before_retry=None):
+        """Run `launch` (library calls on `h`); in 3xf16 mode check the range guard afterwards (one
+        stream sync) and, if it tripped, call `before_retry` and run `launch` again in exact fp32."""
+        if self.precision == "fp32":
+            return launch()
+        L = _lib.lib()
+        s = _lib.stream_ptr(dev)
+        _lib.check(L.ifd_guard_reset(h.h, s))
+        res = launch()
+        tripped = ctypes.c_int()
+        _lib.check(L.ifd_guard_read(h.h, ctypes.byref(tripped), s))
+        if not tripped.value:
+            return res
+        self.guard_trips += 1
+        import warnings
+        warnings.warn("ifd: 3xf16 range guard tripped (a conv operand reached the f16 range); recomputing in fp32")
+        if before_retry is not None:
+            before_retry()
+        prec, self.precision = self.precision, "fp32"  # launch() may re-apply self.precision via handle()
+        _lib.check(L.ifd_set_precision(h.h, _lib.PRECISIONS["fp32"]))
+        try:
+            return launch()
+        finally:
+            self.precision = prec
+            _lib.check(L.ifd_set_precision(h.h, _lib.PRECISIONS[prec]))
 
     def memory(self):
         h = self._handle

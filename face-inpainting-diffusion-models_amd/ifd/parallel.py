@@ -26,12 +26,22 @@ def shard_range(global_batch, rank, world_size):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def device_for(local_rank):
+    """The GPU of a local rank. With fewer GPUs than ranks (a rehearsal of the N-rank path on a
+    smaller box) ranks share devices round-robin and `init` falls back to gloo, since RCCL needs
+    one rank per GPU."""
+    n = torch.cuda.device_count()
+    return torch.device("cuda", local_rank % n) if n else torch.device("cpu")
+
+
 def init(backend=None, device=None):
     """Initialise the default process group when running under torch.distributed.run."""
     rank, ws, local = world()
     if ws > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        if backend is None:
+            shared = torch.cuda.device_count() < int(os.environ.get("LOCAL_WORLD_SIZE", ws))
+            backend = "nccl" if torch.cuda.is_available() and not shared else "gloo"
         if backend == "nccl":
             dist.init_process_group(backend, device_id=device)
         else:
@@ -64,8 +74,10 @@ def gather_images(local, global_batch):
     ws = dist.get_world_size()
     sizes = [shard_range(global_batch, r, ws) for r in range(ws)]
     cap = max(hi - lo for lo, hi in sizes)
-    pad = local.new_zeros((cap,) + tuple(local.shape[1:]))
-    pad[: local.shape[0]] = local
-    out = local.new_empty((ws * cap,) + tuple(local.shape[1:]))
+    src = local if dist.get_backend() == "nccl" else local.cpu()  # gloo: host buffers
+    pad = src.new_zeros((cap,) + tuple(src.shape[1:]))
+    pad[: src.shape[0]] = src
+    out = src.new_empty((ws * cap,) + tuple(src.shape[1:]))
     dist.all_gather_into_tensor(out, pad.contiguous())
-    return torch.cat([out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)], 0)
+    full = torch.cat([out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)], 0)
+    return full.to(local.device)

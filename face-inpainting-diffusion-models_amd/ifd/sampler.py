@@ -13,7 +13,13 @@ float64, rounded to fp32 once when they meet an fp32 tensor.
 
 RNG: every draw happens in reference order on `noise_device` (default: the sampling device, as
 the reference does); `noise_device="cpu"` draws from the global CPU generator and uploads, which
-reproduces CPU-generated golden fixtures bit-for-bit in the noise.
+reproduces CPU-generated golden fixtures bit-for-bit in the noise. `noise_shard=(lo, hi, B)` is
+the multi-GPU parity mode: every draw is made for the FULL batch of B images in
+reference order and rows lo:hi are kept, so a rank's images see exactly the noise they would in an
+unsharded run (results independent of the GPU count).
+
+Shapes: gt must be [B,3,H,W] and masks [B,1,H,W] (1 = hole), or broadcastable to them along the
+batch (a [1,...] tensor is expanded); anything else raises ValueError before a kernel is launched.
 """
 from __future__ import annotations
 
@@ -73,15 +79,36 @@ def ddpm_coeffs(diffusion, i, clip=True):
     return c
 
 
+def prepare_gt_mask(gt, masks, B, H, W, device):
+    """gt -> contiguous fp32 [B,3,H,W], masks -> [B,1,H,W] on `device`; a batch-1 tensor is
+    expanded (the reference broadcasts it). The kernels index exactly these shapes."""
+    gt = torch.as_tensor(gt)
+    masks = torch.as_tensor(masks)
+    if gt.dim() != 4 or gt.shape[1:] != (3, H, W) or gt.shape[0] not in (1, B):
+        raise ValueError(f"gt must be [{B},3,{H},{W}] (or batch 1), got {tuple(gt.shape)}")
+    if masks.dim() != 4 or masks.shape[1:] != (1, H, W) or masks.shape[0] not in (1, B):
+        raise ValueError(f"masks must be [{B},1,{H},{W}] (or batch 1), got {tuple(masks.shape)}")
+    gt = gt.to(device=device, dtype=torch.float32).expand(B, 3, H, W).contiguous()
+    masks = masks.to(device=device, dtype=torch.float32).expand(B, 1, H, W).contiguous()
+    return gt, masks
+
+
 class InpaintingSampler:
     """Sampling core of the reference's `InpaintingSampler` (no dataset / metrics / IO)."""
 
-    def __init__(self, model, diffusion, ddim_timesteps=100, device=None, noise_device=None, args=None):
+    def __init__(self, model, diffusion, ddim_timesteps=100, device=None, noise_device=None, args=None,
+                 noise_shard=None):
         self.model = model
         self.diffusion = diffusion
         self.args = args if args is not None else SimpleNamespace(ddim_timesteps=ddim_timesteps)
         self.device = device if device is not None else next(model.parameters()).device
         self.noise_device = noise_device
+        if noise_shard is not None:
+            lo, hi, gb = (int(v) for v in noise_shard)
+            if not 0 <= lo < hi <= gb:
+                raise ValueError(f"noise_shard must satisfy 0 <= lo < hi <= B, got {noise_shard}")
+            noise_shard = (lo, hi, gb)
+        self.noise_shard = noise_shard
 
     # code/test_inp_ddim_50.py:373-385
     def model_fn(self, x, t, gt=None, gt_keep_mask=None, **kwargs):
@@ -102,6 +129,12 @@ class InpaintingSampler:
     # ---- RNG in reference order -------------------------------------------------------------
     def _randn(self, shape, device):
         nd = self.noise_device
+        if self.noise_shard is not None:
+            lo, hi, gb = self.noise_shard
+            if shape[0] != hi - lo:
+                raise ValueError(f"batch {shape[0]} does not match noise_shard rows {lo}:{hi}")
+            full = torch.randn(gb, *shape[1:], device=nd if nd is not None else device)
+            return full[lo:hi].to(device).contiguous()
         if nd is None or torch.device(nd) == torch.device(device):
             return torch.randn(*shape, device=device)
         return torch.randn(*shape, device=nd).to(device, non_blocking=True)
@@ -110,23 +143,45 @@ class InpaintingSampler:
         return (getattr(model_fn, "__self__", None) is self and getattr(model_fn, "__func__", None)
                 is InpaintingSampler.model_fn and isinstance(self.model, DiffusionInpaintingModel))
 
+    def _guarded(self, model_fn, device, run):
+        """The fused loops in 3xf16 mode: one range-guard check at the end of the loop (one sync);
+        if an operand reached the f16 range, the RNG state is rewound and the loop re-run in exact
+        fp32, so the returned sample is what the fp32 path would give for the same seed."""
+        if not (self._fused(model_fn) and self.model.precision != "fp32"):
+            return run()
+        dev = torch.device(device)
+        states = [(None, torch.get_rng_state())]
+        if dev.type == "cuda":
+            states.append((dev, torch.cuda.get_rng_state(dev)))
+
+        def rewind():
+            for d, st in states:
+                if d is None:
+                    torch.set_rng_state(st)
+                else:
+                    torch.cuda.set_rng_state(st, d)
+        return self.model.run_guarded(self.model.handle(dev), dev, run, before_retry=rewind)
+
     # ---- script DDIM (code/test_inp_ddim_50.py:470-576) -------------------------------------
     def inpainting_ddim_sample_loop(self, model_fn, shape, gt_images, masks, clip_denoised=True, device=None,
                                     progress=False, eta=0.0):
         if device is None:
             device = next(self.model.parameters()).device
+        return self._guarded(model_fn, device, lambda: self._ddim_loop(model_fn, shape, gt_images, masks,
+                                                                       clip_denoised, device, progress, eta))
+
+    def _ddim_loop(self, model_fn, shape, gt_images, masks, clip_denoised, device, progress, eta):
         assert isinstance(shape, (tuple, list))
+        B, _, H, W = shape
+        gt, mk = prepare_gt_mask(gt_images, masks, B, H, W, device)
         img = self._randn(shape, device).contiguous()
         seq = self.create_ddim_timestep_sequence(self.diffusion.num_timesteps, self.args.ddim_timesteps)
         it = enumerate(seq)
         if progress:
             from tqdm import tqdm
             it = tqdm(it, total=len(seq), desc=f"DDIM inpainting ({self.args.ddim_timesteps} steps)")
-        gt = gt_images.to(device=device, dtype=torch.float32).contiguous()
-        mk = masks.to(device=device, dtype=torch.float32).contiguous()
         fused = self._fused(model_fn)
         L = _lib.lib()
-        B, _, H, W = shape
         h = self.model.handle(torch.device(device)) if fused else None
         keep = None if fused else 1 - mk
         for k, tau in it:
@@ -141,9 +196,9 @@ class InpaintingSampler:
                     _lib.check(L.ifd_ddim_step(h.h, _lib.ptr(t), B, H, W, _lib.ptr(img), _lib.ptr(gt), _lib.ptr(mk),
                                                _lib.ptr(noise), _lib.ptr(known), c, _lib.stream_ptr(device)))
                 else:
-                    out = out.contiguous()
-                    if out.shape[1] not in (3, 6):
-                        raise ValueError(f"Unexpected model output shape: {out.shape}")
+                    out = out.to(torch.float32).contiguous()
+                    if out.dim() != 4 or out.shape[0] != B or out.shape[1] not in (3, 6) or out.shape[2:] != (H, W):
+                        raise ValueError(f"Unexpected model output shape: {tuple(out.shape)}")
                     if out.shape[1] == 3:
                         out = torch.cat([out, torch.zeros_like(out)], 1)
                     _lib.check(L.ifd_ddim_update(_lib.ptr(out), B, H, W, _lib.ptr(img), _lib.ptr(gt), _lib.ptr(mk),
@@ -156,17 +211,20 @@ class InpaintingSampler:
                                  progress=False):
         if device is None:
             device = next(self.model.parameters()).device
+        return self._guarded(model_fn, device, lambda: self._ddpm_loop(model_fn, shape, gt_images, masks,
+                                                                       clip_denoised, device, progress))
+
+    def _ddpm_loop(self, model_fn, shape, gt_images, masks, clip_denoised, device, progress):
         assert isinstance(shape, (tuple, list))
+        B, _, H, W = shape
+        gt, mk = prepare_gt_mask(gt_images, masks, B, H, W, device)
         img = self._randn(shape, device).contiguous()
         indices = list(range(self.diffusion.num_timesteps))[::-1]
         if progress:
             from tqdm import tqdm
             indices = tqdm(indices, desc="DDPM inpainting with injection")
-        gt = gt_images.to(device=device, dtype=torch.float32).contiguous()
-        mk = masks.to(device=device, dtype=torch.float32).contiguous()
         fused = self._fused(model_fn)
         L = _lib.lib()
-        B, _, H, W = shape
         h = self.model.handle(torch.device(device)) if fused else None
         keep = None if fused else 1 - mk
         for i in indices:
@@ -180,7 +238,9 @@ class InpaintingSampler:
                     _lib.check(L.ifd_ddpm_step(h.h, _lib.ptr(t), B, H, W, _lib.ptr(img), _lib.ptr(gt), _lib.ptr(mk),
                                                _lib.ptr(noise), _lib.ptr(known), c, _lib.stream_ptr(device)))
                 else:
-                    out = out.contiguous()
+                    out = out.to(torch.float32).contiguous()
+                    if tuple(out.shape) != (B, 6, H, W):  # p_mean_variance's LEARNED_RANGE split (:241-243)
+                        raise ValueError(f"DDPM needs a [B,6,H,W] model output, got {tuple(out.shape)}")
                     _lib.check(L.ifd_ddpm_update(_lib.ptr(out), B, H, W, _lib.ptr(img), _lib.ptr(gt), _lib.ptr(mk),
                                                  _lib.ptr(noise), _lib.ptr(known), c, _lib.stream_ptr(device)))
                 del noise, known
@@ -189,11 +249,12 @@ class InpaintingSampler:
     @staticmethod
     def final_blend(result, gt_images, masks):
         """code/test_inp_ddim_50.py:692-696 (one HIP kernel)."""
-        r = result.contiguous()
-        g = gt_images.to(r.device, torch.float32).contiguous()
-        m = masks.to(r.device, torch.float32).contiguous()
-        out = torch.empty_like(r)
+        r = result.to(torch.float32).contiguous()
+        if r.dim() != 4 or r.shape[1] != 3:
+            raise ValueError(f"result must be [B,3,H,W], got {tuple(r.shape)}")
         B, C, H, W = r.shape
+        g, m = prepare_gt_mask(gt_images, masks, B, H, W, r.device)
+        out = torch.empty_like(r)
         _lib.check(_lib.lib().ifd_blend(_lib.ptr(r), _lib.ptr(g), _lib.ptr(m), B, C, H, W, _lib.ptr(out),
                                         _lib.stream_ptr(r.device)))
         return out

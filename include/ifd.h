@@ -78,7 +78,27 @@ int ifd_finalize(ifd_handle* h);
 #define IFD_PREC_FP32 0
 #define IFD_PREC_3XF16 1
 int ifd_set_precision(ifd_handle* h, int prec);
+/* 3xf16 range guard. The split needs every conv operand below the f16 range (|a| < 65504; the
+ * weights are checked at finalize). The 3xf16 kernels set a device word when an operand reaches it
+ * (activations in the producers, the raw 1x1-skip residual stream in the consumers). reset: async
+ * on `stream`; read: synchronises `stream`, *tripped = 1 if any launch since the reset saw an
+ * out-of-range operand — that eval's output is not fp32-accurate and must be recomputed in
+ * IFD_PREC_FP32 (ifd.model / ifd.sampler do this automatically). */
+int ifd_guard_reset(ifd_handle* h, void* stream);
+int ifd_guard_read(ifd_handle* h, int* tripped, void* stream);
 int ifd_get_precision(ifd_handle* h, int* prec);
+/* Handle options. No reference counterpart: execution choices of this library that never change
+ * the arithmetic of a single image except where noted. Initial values are read from the
+ * environment once, in ifd_create (IFD_BATCH_INVARIANT, IFD_CONV_STREAM, IFD_GN_FUSED, IFD_X3_OFF,
+ * IFD_STREAM_CW, IFD_CONV_BM=128, IFD_CONV_LDS_PAD); nothing is read per launch. Keys:
+ *   "batch_invariant" 0/1  tile kind and split-K chosen per image, so an image's output is
+ *                          bit-identical whatever batch it shares a launch with (multi-GPU parity
+ *                          mode: N ranks x B/N images == one rank x B images). Slower on small layers.
+ *   "conv_stream"     0..2 wide fp32 layers: one tile per workgroup / persistent 1 or 2 per CU
+ *   "gn_fused"        0/1  GroupNorm statistics fused into the producing conv (1) or a separate pass
+ *   "x3_off", "stream_cw", "conv_bm128", "lds_pad"   development switches (bisecting, tuning) */
+int ifd_set_option(ifd_handle* h, const char* key, int value);
+int ifd_get_option(ifd_handle* h, const char* key, int* value);
 /* Bytes of device workspace the handle holds (weights + activations). */
 int ifd_memory(ifd_handle* h, int64_t* weight_bytes, int64_t* workspace_bytes);
 

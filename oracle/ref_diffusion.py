@@ -22,7 +22,8 @@ Reference citations (paths relative to the reference repository root):
   code/test_inp_ddim_50.py:692-696    final blend
 
 RNG: every draw uses the global torch CPU generator in exactly the reference's call order,
-so fixtures regenerate bit-identically from a seed.
+so fixtures regenerate bit-identically from a seed. Draws are always fp32 (`_randn`), so an fp64
+model (the error-envelope fixtures) sees the same noise values as the fp32 reference.
 """
 from __future__ import annotations
 
@@ -118,6 +119,11 @@ def ddim_timestep_sequence(T, n):
     return seq[::-1]
 
 
+def _randn(like):
+    """torch.randn_like for an fp32 tensor; fp32 draws cast up for an fp64 one."""
+    return torch.randn(like.shape).to(like.dtype)
+
+
 def script_ddim_loop(tb, model_fn, shape, gt, masks, ddim_steps, clip=True, eta=0.0):
     """code/test_inp_ddim_50.py:470-576 (post-update injection at alpha_prev, fresh noise)."""
     img = torch.randn(*shape)
@@ -134,10 +140,10 @@ def script_ddim_loop(tb, model_fn, shape, gt, masks, ddim_steps, clip=True, eta=
             x0 = torch.clamp(x0, -1, 1)
         sigma = eta * torch.sqrt((1 - a_p) / (1 - a_t)) * torch.sqrt(1 - a_t / a_p)
         pred_dir = torch.sqrt(1 - a_p - sigma ** 2) * eps
-        noise = torch.randn_like(img) if tau > 0 and eta > 0 else torch.zeros_like(img)
+        noise = _randn(img) if tau > 0 and eta > 0 else torch.zeros_like(img)
         img = torch.sqrt(a_p) * x0 + pred_dir + sigma * noise
         if tau > 0:
-            known = torch.randn_like(gt)
+            known = _randn(gt)
             img = img * masks + (torch.sqrt(a_p) * gt + torch.sqrt(1 - a_p) * known) * keep
     return img
 
@@ -149,12 +155,12 @@ def script_ddpm_loop(tb, model_fn, shape, gt, masks, clip=True):
     for i in range(tb.T)[::-1]:
         t = torch.tensor([i] * shape[0])
         out = p_mean_variance(tb, model_fn, img, t, clip, {"gt": gt, "gt_keep_mask": keep})
-        noise = torch.randn_like(img)
+        noise = _randn(img)
         nonzero = (t != 0).float().view(-1, 1, 1, 1)
         img = out["mean"] + nonzero * torch.exp(0.5 * out["log_variance"]) * noise
         if i > 0:
             a = torch.tensor(tb.ac[i - 1])
-            known = torch.randn_like(gt)
+            known = _randn(gt)
             img = img * masks + (torch.sqrt(a) * gt + torch.sqrt(1 - a) * known) * keep
     return img
 

@@ -37,3 +37,38 @@ def loops():
 @pytest.fixture(scope="session")
 def layers():
     return dict(np.load(os.path.join(GOLDEN, "layers.npz")))
+
+
+@pytest.fixture(scope="session")
+def meta_full():
+    with open(os.path.join(GOLDEN, "full", "meta_full.json")) as f:
+        return json.load(f)
+
+
+def golden_full(name):
+    return dict(np.load(os.path.join(GOLDEN, "full", f"{name}.npz")))
+
+
+_RECORDED = {}
+
+
+@pytest.fixture(scope="session")
+def record():
+    """record(key, **numbers): measured parity errors, written at session end to
+    $IFD_PARITY_JSON (default gpurun_out/parity.json when gpurun_out/ exists) so the numbers the
+    gates check are kept, not only printed."""
+    def rec(key, **vals):
+        _RECORDED[key] = {k: (float(v) if isinstance(v, (int, float, np.floating)) else v) for k, v in vals.items()}
+        print(key, _RECORDED[key])
+    yield rec
+    path = os.environ.get("IFD_PARITY_JSON")
+    if not path and os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        path = os.path.join(ROOT, "gpurun_out", "parity.json")
+    if path and _RECORDED:
+        old = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                old = json.load(f)
+        old.update(_RECORDED)
+        with open(path, "w") as f:
+            json.dump(old, f, indent=1, sort_keys=True)

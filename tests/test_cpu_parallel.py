@@ -55,3 +55,60 @@ def test_gather_and_max_gloo(gb):
     for rank, vals, t in out:
         assert vals == [float(i) for i in range(gb)]
         assert t == 2.0
+
+
+def _noise_worker(rank, ws, port, gb, q):
+    """Parity mode: each rank's sampler draws for the full batch in reference order and
+    keeps its rows; gathered, the ranks' draws equal one unsharded run's."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(ws), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from ifd import parallel
+    from ifd.sampler import InpaintingSampler
+    parallel.init(backend="gloo")
+    lo, hi = parallel.shard_range(gb, rank, ws)
+    s = InpaintingSampler(None, None, device=torch.device("cpu"), noise_device="cpu", noise_shard=(lo, hi, gb))
+    torch.manual_seed(42)
+    draws = [s._randn((hi - lo, 3, 8, 8), "cpu") for _ in range(3)]  # img, then per-step noise / known
+    full = [parallel.gather_images(d, gb) for d in draws]
+    q.put((rank, [f.tolist() for f in full]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("gb", [4, 5])
+def test_noise_shard_matches_full_batch_gloo(gb):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_noise_worker, args=(r, 2, port, gb, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    torch.manual_seed(42)
+    ref = [torch.randn(gb, 3, 8, 8) for _ in range(3)]
+    for rank, full in out:
+        for f, r in zip(full, ref):
+            assert torch.equal(torch.tensor(f), r)
+
+
+def test_noise_shard_rejects_mismatched_batch():
+    from ifd.sampler import InpaintingSampler
+    s = InpaintingSampler(None, None, device=torch.device("cpu"), noise_shard=(2, 4, 8))
+    with pytest.raises(ValueError):
+        s._randn((3, 3, 8, 8), "cpu")
+    with pytest.raises(ValueError):
+        InpaintingSampler(None, None, device=torch.device("cpu"), noise_shard=(4, 2, 8))
+
+
+def test_prepare_gt_mask_broadcasts_and_rejects():
+    from ifd.sampler import prepare_gt_mask
+    gt = torch.rand(1, 3, 8, 8)
+    m = torch.ones(1, 1, 8, 8)
+    g2, m2 = prepare_gt_mask(gt, m, 4, 8, 8, "cpu")
+    assert g2.shape == (4, 3, 8, 8) and m2.shape == (4, 1, 8, 8) and g2.is_contiguous()
+    assert torch.equal(g2[3], gt[0])
+    for bad_gt, bad_m in ((torch.rand(2, 3, 8, 8), m), (gt, torch.ones(4, 3, 8, 8)), (gt, torch.ones(4, 1, 4, 4))):
+        with pytest.raises(ValueError):
+            prepare_gt_mask(bad_gt, bad_m, 4, 8, 8, "cpu")
