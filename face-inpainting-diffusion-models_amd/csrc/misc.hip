@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ i
         for (int g = 0; g < SK_NB / 4; ++g) {
           const f32x4 s = s4[g];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) acc[4 * g + c] += w * s[c];
+          for (int c = 0; c < 4; ++c) acc[4 * g + c] = fmaf(w, s[c], acc[4 * g + c]);  // one rounding in every slot
         }
       }
     }

@@ -11,9 +11,11 @@ Differences, all deliberate:
     bias default-initialised from the global torch RNG (U(+-1/sqrt(fan_in)), as nn.Conv2d does —
     the exact RNG stream of the reference's module construction is not reproduced).
   * `noise_schedule` / `steps` are keyword overrides (defaults = the reference factory's).
-  * `precision` selects the conv arithmetic ("fp32": exact fp32 MFMA; "3xf16": the fp32-accurate
-    split mode); default from the IFD_PRECISION environment variable, else "fp32",
-    so the reference's scripts can switch without edits.
+  * `precision` selects the conv arithmetic ("3xf16": the split mode, DESIGN.md §3a, whose error
+    against exact arithmetic matches the reference's own fp32 — tests/test_gpu_full.py — and whose
+    range guard recomputes any out-of-range eval in fp32; "fp32": the plain fp32 MFMA chain);
+    default from the IFD_PRECISION environment variable, else "3xf16", so the reference's scripts
+    can switch without edits.
 """
 from __future__ import annotations
 
@@ -39,7 +41,7 @@ def _unwrap(ckpt):
 def create_model_and_diffusion(checkpoint_path, device, img_size=256, *, steps=1000, noise_schedule="quadratic",
                                model_channels=128, seed=1, precision=None):
     cfg = UNetConfig(image_size=img_size, model_channels=model_channels)
-    precision = precision or os.environ.get("IFD_PRECISION", "fp32")
+    precision = precision or os.environ.get("IFD_PRECISION", "3xf16")
     model = DiffusionInpaintingModel(cfg, device=device, precision=precision)
     if checkpoint_path is None:
         sd = make_state_dict(cfg, seed=seed, prefix="base_model.")

@@ -180,7 +180,7 @@ class LibraryState:
     def gt_noised(self, gt, tau):
         key = (tuple(gt.shape), tau)
         if key not in self.cache:
-            self.cache[key] = torch.randn_like(gt)
+            self.cache[key] = _randn(gt)
         t = torch.tensor([tau]).expand(gt.shape[0])
         return q_sample(self.tb, gt, t, self.cache[key])
 
@@ -195,7 +195,7 @@ class LibraryState:
             w = self.gt_noised(gt, tau)
         else:
             ac = extract(self.tb.ac, t, x.shape)
-            w = torch.sqrt(ac) * gt + torch.sqrt(1 - ac) * torch.randn_like(gt)
+            w = torch.sqrt(ac) * gt + torch.sqrt(1 - ac) * _randn(gt)
         if keep.shape[1] == 1 and x.shape[1] > 1:
             keep = keep.repeat(1, x.shape[1], 1, 1)
         return keep * w + (1 - keep) * x
@@ -215,7 +215,7 @@ def library_ddim_loop(tb, model, shape, model_kwargs, eta=0.0, clip=True, inject
         ab = extract(tb.ac, t, x.shape)
         abp = extract(tb.ac_prev, t, x.shape)
         sigma = eta * torch.sqrt((1 - abp) / (1 - ab)) * torch.sqrt(1 - ab / abp)
-        nz = torch.randn_like(x)
+        nz = _randn(x)
         mean = out["pred_xstart"] * torch.sqrt(abp) + torch.sqrt(1 - abp - sigma ** 2) * eps
         nonzero = (t != 0).float().view(-1, 1, 1, 1)
         img = mean + nonzero * sigma * nz
@@ -232,7 +232,7 @@ def library_ddpm_loop(tb, model, shape, model_kwargs, clip=True, injection=True,
         if injection and model_kwargs:
             x = st.inject(x, t, model_kwargs["gt"], model_kwargs["gt_keep_mask"], schedule, cumulative)
         out = p_mean_variance(tb, model, x, t, clip, model_kwargs)
-        nz = torch.randn_like(x)
+        nz = _randn(x)
         nonzero = (t != 0).float().view(-1, 1, 1, 1)
         img = out["mean"] + nonzero * torch.exp(0.5 * out["log_variance"]) * nz
     return img

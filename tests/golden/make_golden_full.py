@@ -156,6 +156,26 @@ def case_adv(ref, rec):
                                                           use_ddim=use_ddim, eta=eta, progress=False,
                                                           device=torch.device("cpu"), injection_schedule=sched_inj,
                                                           use_cumulative_noise=cum)
+        # the oracle's library loop with the same arguments: fp32 (must equal the reference) and
+        # fp64 (the envelope)
+        tb = ref_diffusion.Tables(ref_diffusion.get_named_beta_schedule("cosine", 40))
+        kw = {"gt": gt, "gt_keep_mask": keep, "masked_image": gt * keep, "mask": 1 - keep}
+        for dt, tag in ((torch.float32, "y32"), (torch.float64, "y64")):
+            sdo = {k: v.to(dt) for k, v in ref_unet.strip_prefix(sd).items()}
+
+            def omodel(x, t, masked_image=None, mask=None, **_):
+                return ref_unet.inpaint_forward(sdo, x, t, masked_image, mask, REDUCED)
+            loop = ref_diffusion.library_ddim_loop if use_ddim else ref_diffusion.library_ddpm_loop
+            extra = dict(eta=eta) if use_ddim else {}
+            torch.manual_seed(77)
+            with torch.no_grad():
+                yo = loop(tb, omodel, (2, 3, 64, 64), kw, schedule=sched_inj, cumulative=cum, **extra)
+            if tag == "y32":
+                rec["checks"][f"oracle_vs_ref_{name}"] = mg.maxabs(y, yo)
+            else:
+                rec["envelopes"][name] = _stats(y, yo)
+                arrs[f"{name}/y64"] = yo.numpy()
+        print(f"[full] {name}: oracle {rec['checks'][f'oracle_vs_ref_{name}']:.3g} env {rec['envelopes'][name]}")
         arrs[f"{name}/y"] = y.numpy()
         arrs[f"{name}/gt"] = gt.numpy()
         arrs[f"{name}/mask"] = mask.numpy()
