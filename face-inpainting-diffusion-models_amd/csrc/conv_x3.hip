@@ -268,12 +268,14 @@ struct XProducer {
     }
   }
 
-  __device__ __forceinline__ void load(Set& s, const ConvParams& p, int c, int nmain, int nskip) {
+  // ism: a 3x3 chunk (idx = its 16-channel chunk of the main input) or a 1x1 skip chunk (idx =
+  // its chunk of the skip input); see KCursor for the order
+  __device__ __forceinline__ void load(Set& s, const ConvParams& p, bool ism, int idx) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) s.vld[i] = valid[i];
     if (X3_ABLATE == 1 || X3_ABLATE >= 8) return;
-    if (SKIP && c >= nmain) return;  // operand by DMA (see dma)
-    const int cb0 = 16 * c;
+    if (SKIP && !ism) return;  // operand by DMA (see dma)
+    const int cb0 = 16 * idx;
     if (cb0 < p.c0) {
 #pragma unroll
       for (int i = 0; i < IT; ++i) {
@@ -300,11 +302,12 @@ struct XProducer {
   //     XSKA, 16 pixels per round (4 lanes per pixel: 16 cache lines per wave-instruction), the
   //     lane's 16-B quad slot XOR-swizzled by (pixel >> 2) & 3 so the consumers' ds_read_b128 are
   //     conflict-free.
-  __device__ __forceinline__ void dma(const ConvParams& p, int ct, int c, int nmain, int nskip, lds_f* Wslot) const {
+  __device__ __forceinline__ void dma(const ConvParams& p, int ct, bool ism, int idx, int nmain, int nskip,
+                                      lds_f* Wslot) const {
     if (X3_ABLATE == 5 || X3_ABLATE >= 8) return;
     const int pw = __builtin_amdgcn_readfirstlane(ptid >> 6);
-    if (SKIP && c >= nmain) {
-      const int kk = c - nmain;
+    if (SKIP && !ism) {
+      const int kk = idx;
       const rsrc_t r = mkrsrc(p.wskip + ((size_t)ct * nskip + kk) * (XW / 9));
       const int qb = pw * 64;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(Wslot + 4 * qb), 16,
@@ -327,7 +330,7 @@ struct XProducer {
     // per-lane offset = the loop-invariant 16 * lane (lane16), the round in the scalar offset: a
     // per-round VALU temporary would share VGPRs with in-flight halo loads and make the compiler
     // wait for them (vmcnt) before the DMA issues
-    const rsrc_t r = mkrsrc(p.wpack + ((size_t)ct * nmain + c) * XW);
+    const rsrc_t r = mkrsrc(p.wpack + ((size_t)ct * nmain + idx) * XW);
 #pragma unroll
     for (int i = 0; i < XWDMA; ++i) {
       const int qb = (i * 4 + pw) * 64;
@@ -482,6 +485,28 @@ __device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* A
 #pragma unroll
     for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(al[mr], bs[nr], acc[mr][nr]);
 }
+
+// Order of a unit's K stream: the 3x3 chunks, then the 1x1 skip chunks. (Measured alternative,
+// r02: interleaving the skip chunks among the 3x3 chunks in proportion made the skip layers 18 %
+// SLOWER — each 3x3 chunk's prologue VALU, done by the producers one interval ahead, then lands in
+// a short skip interval with no MFMA work to hide behind, once per 3x3 chunk instead of once per
+// unit.)
+struct KCursor {
+  int mi, si;
+  __device__ __forceinline__ void reset() { mi = si = 0; }
+  // kind of the chunk at stream position c (in order, one call per position); idx = its index
+  __device__ __forceinline__ bool next(int c, int S, int nmain, int nskip, int& idx) {
+    if (S > 1) {  // a split-K unit starts mid-stream
+      const bool m = c < nmain;
+      idx = m ? c : c - nmain;
+      return m;
+    }
+    (void)nskip;
+    const bool m = mi < nmain;  // 3x3 chunks first, then the 1x1 skip chunks
+    idx = m ? mi++ : si++;
+    return m;
+  }
+};
 
 template <int XF, bool SKIP, int TW>
 __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
@@ -647,15 +672,19 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     XBARRIER_CONSUMER();  // chunk 0 staged
     float gmax = 0.f;
     int kk = 0, u = 0, z = 0;
+    KCursor kc;
     STile t = unit_of(0, z);
     for (int j = 0; j < J; ++j) {
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
         p.trace[64 * blockIdx.x + j] = __builtin_amdgcn_s_memtime();
       const lds_f* Ws = W0 + (j % 3) * XW;
-      const int c = z * nchu + kk;  // chunk index within the tile's K stream
+      const int c = z * nchu + kk;  // chunk position within the tile's K stream
+      if (kk == 0) kc.reset();
+      int cidx;
+      const bool cmain = kc.next(c, S, nmain, nskip, cidx);
       if (kk == nchu - 1 && S == 1 && X3_ABLATE < 9) prefetch(t);
       if (X3_ABLATE == 4) {
-      } else if (!SKIP || c < nmain) {
+      } else if (!SKIP || cmain) {
         consume_x3<TW>(acc, A0 + (j & 1) * XA, Ws, pb);
       } else {
         consume_skip(acc, Ws + XSKA, Ws, pbs, gmax);
@@ -691,13 +720,19 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   int jl = 0, ul = 0, kl = 0, zl = 0;
   STile tl = unit_of(0, zl);
   int lastmain = 1, prevmain = 1;  // the last / the previous issued chunk is a 3x3 chunk
+  KCursor pc;
+  int cmain = 1, cidx = 0;  // kind / index of the cursor's chunk (kept for the clamped repeats)
   auto issue = [&](typename XProducer<XF, SKIP, TW>::Set& s) {  // DMA + register loads of the cursor's chunk, then advance
-    const int c = __builtin_amdgcn_readfirstlane(zl * nchu + kl);
+    if (jl < J) {
+      const int c = __builtin_amdgcn_readfirstlane(zl * nchu + kl);
+      if (kl == 0) pc.reset();
+      cmain = pc.next(c, S, nmain, nskip, cidx) ? 1 : 0;
+    }
     prevmain = lastmain;
-    lastmain = (!SKIP || c < nmain) ? 1 : 0;
+    lastmain = (!SKIP || cmain) ? 1 : 0;
     P.enter(p, tl, ul);
-    P.dma(p, tl.ct, c, nmain, nskip, W0 + (jl % 3) * XW);
-    P.load(s, p, c, nmain, nskip);
+    P.dma(p, tl.ct, cmain, cidx, nmain, nskip, W0 + (jl % 3) * XW);
+    P.load(s, p, cmain, cidx);
     if (jl + 1 < J) {
       ++jl;
       if (++kl == nchu) {

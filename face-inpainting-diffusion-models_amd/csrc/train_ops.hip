@@ -1,0 +1,1000 @@
+// Training step ops (BASELINE configs[4]): the fp32 forward pieces the
+// backward needs saved, and every backward kernel of the 9-channel UNet — conv dgrad (the forward
+// fp32 MFMA conv on transposed-flipped weights) and wgrad (fp32 MFMA over pixels), GroupNorm +
+// scale/shift + SiLU backward, nearest-up / avg-pool backward, QKV attention backward, the
+// time-embedding linears, the masked eps-MSE loss and its gradient, grad-norm clipping and AdamW.
+// Reference: code/train_inpainting.py:15-79 (train_epoch: loss.backward, clip_grad_norm_(1.0),
+// AdamW.step), code/gaussian_diffusion.py:540-614 (training_losses), code/nn.py / code/unet.py
+// (the modules differentiated). Activations are NHWC fp32; weights live in the reference's
+// torch layouts inside one flat parameter buffer (ifd/train.py) and are packed per step.
+// Every reduction runs in a fixed order (no atomics): a step is bit-reproducible.
+#include "../../include/ifd_train.h"
+
+#include <cmath>
+#include <cstring>
+
+#include "conv.h"
+#include "conv_dev.h"
+#include "kernels.h"
+
+namespace ifd {
+namespace {
+
+constexpr int TB = 256;
+
+inline int grid1(int64_t n, int per = TB) { return (int)((n + per - 1) / per); }
+
+// ---------------------------------------------------------------------------------------------
+// Weight packing on the device (weights change every step). Layout of conv.hip:
+// [Cout_pad/BN][Cin_pad/8][taps][q=2][BN][4], element W'[ct*BN + col][ch*8 + q*4 + j][tap].
+// cout / cin are the weight tensor's dims W[cout][cin][taps]; cin_pad / cout_pad the packed conv's.
+// transpose = 0: W' = W (forward). transpose = 1: dgrad, W'[ci][co][tap] = W[co][ci][taps-1-tap]
+// (the transposed convolution of a stride-1, pad-1 3x3 conv is a 3x3 conv with the kernel flipped).
+__global__ void pack_conv_kernel(const float* __restrict__ w, int cout, int cin, int taps, int bn, int cin_pad,
+                                 int cout_pad, int transpose, float* __restrict__ dst) {
+  const int64_t tot = (int64_t)cout_pad * cin_pad * taps;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  // decode the destination index
+  const int jj = (int)(i & 3);
+  int64_t r = i >> 2;
+  const int col = (int)(r % bn);
+  r /= bn;
+  const int q = (int)(r & 1);
+  r >>= 1;
+  const int tap = (int)(r % taps);
+  r /= taps;
+  const int nch = cin_pad / 8;
+  const int chk = (int)(r % nch);
+  const int ct = (int)(r / nch);
+  const int o = ct * bn + col, c = chk * 8 + q * 4 + jj;  // packed (out, in) channel
+  float v = 0.f;
+  if (transpose == 0) {
+    if (o < cout && c < cin) v = w[((size_t)o * cin + c) * taps + tap];
+  } else {  // packed out channel o = the forward's input channel, packed in channel c = its output
+    if (o < cin && c < cout) v = w[((size_t)c * cin + o) * taps + (taps - 1 - tap)];
+  }
+  dst[i] = v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradient on fp32 MFMA (v_mfma_f32_32x32x2f32):
+//   dW[co][ci][tap] = sum over pixels (n, y, x) of dY[n,y,x,co] * X[n, y + ky - 1, x + kx - 1, ci]
+// with X = concat(x0, x1) along channels, zero padding. GEMM view: M = co, N = ci (one tap per
+// block), K = pixels. Block = 4 waves, tile 64 co x 64 ci; wave w owns rows 32 (w & 1), cols
+// 32 (w >> 1). Per chunk of 32 pixels the block stages dY^T [64][32] and X^T [64][32] (pixel
+// contiguous) in LDS; an MFMA's k pair is pixels (j, 16 + j) so a lane reads its 16 pixels with
+// four ds_read_b128. K is split over blockIdx.y: the partial sums go to slab z of `part`
+// [S][cout][cin][taps] and wgrad_reduce adds the slabs in order (deterministic).
+constexpr int WG_CH = 32;     // pixels per chunk
+constexpr int WG_LD = 36;     // LDS row stride (floats): 16-B aligned rows
+struct WgArgs {
+  const float* dy; int cout;
+  const float* x0; int c0;
+  const float* x1; int c1;
+  int N, H, W, taps;
+  int64_t P;           // N * H * W
+  int chunks_per_split;
+  float* part;         // [S][cout][cin][taps]
+};
+
+__global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
+  __shared__ __attribute__((aligned(16))) float dyt[64 * WG_LD];
+  __shared__ __attribute__((aligned(16))) float xt[64 * WG_LD];
+  const int cin = a.c0 + a.c1;
+  const int nci = (cin + 63) / 64;
+  int b = blockIdx.x;
+  const int tap = b % a.taps;
+  b /= a.taps;
+  const int cit = b % nci, cot = b / nci;
+  const int co0 = cot * 64, ci0 = cit * 64;
+  const int ky = a.taps == 9 ? tap / 3 - 1 : 0, kx = a.taps == 9 ? tap % 3 - 1 : 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int wr = 32 * (wave & 1), wc = 32 * (wave >> 1);
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int64_t nch = (a.P + WG_CH - 1) / WG_CH;
+  const int64_t c_beg = (int64_t)blockIdx.y * a.chunks_per_split;
+  const int64_t c_end = c_beg + a.chunks_per_split < nch ? c_beg + a.chunks_per_split : nch;
+  const int HW = a.H * a.W;
+  // staging assignment: thread -> (pixel pr = tid / 16 and pr + 16, channel quad 4 (tid % 16))
+  const int pr = tid >> 4, cq = 4 * (tid & 15);
+  for (int64_t ch = c_beg; ch < c_end; ++ch) {
+    const int64_t p0 = ch * WG_CH;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int pl = pr + 16 * half;
+      const int64_t pix = p0 + pl;
+      f32x4 vy = {0.f, 0.f, 0.f, 0.f}, vx = {0.f, 0.f, 0.f, 0.f};
+      if (pix < a.P) {
+        const int co = co0 + cq;
+        if (co < a.cout) {
+          if (co + 3 < a.cout && (a.cout & 3) == 0) {
+            vy = *reinterpret_cast<const f32x4*>(a.dy + pix * a.cout + co);
+          } else {
+            for (int j = 0; j < 4; ++j)
+              if (co + j < a.cout) vy[j] = a.dy[pix * a.cout + co + j];
+          }
+        }
+        const int n = (int)(pix / HW), rem = (int)(pix - (int64_t)n * HW);
+        const int y = rem / a.W + ky, x = rem % a.W + kx;
+        const int ci = ci0 + cq;
+        if (y >= 0 && y < a.H && x >= 0 && x < a.W && ci < cin) {
+          const int64_t sp = ((int64_t)n * a.H + y) * a.W + x;
+          for (int j = 0; j < 4; ++j) {
+            const int c = ci + j;
+            if (c < a.c0) vx[j] = a.x0[sp * a.c0 + c];
+            else if (c < cin) vx[j] = a.x1[sp * a.c1 + (c - a.c0)];
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dyt[(cq + j) * WG_LD + pl] = vy[j];
+        xt[(cq + j) * WG_LD + pl] = vx[j];
+      }
+    }
+    __syncthreads();
+    f32x4 av[4], bv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      av[k] = *reinterpret_cast<const f32x4*>(&dyt[(wr + l32) * WG_LD + 16 * h + 4 * k]);
+      bv[k] = *reinterpret_cast<const f32x4*>(&xt[(wc + l32) * WG_LD + 16 * h + 4 * k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[k][j], bv[k][j], acc, 0, 0, 0);
+    __syncthreads();
+  }
+  // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci)
+  float* slab = a.part + (size_t)blockIdx.y * a.cout * cin * a.taps;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int co = co0 + wr + 8 * (r >> 2) + 4 * h + (r & 3);
+    const int ci = ci0 + wc + l32;
+    if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * a.taps + tap] = acc[r];
+  }
+}
+
+__global__ void slab_reduce_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out,
+                                   int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = part[i];
+  for (int z = 1; z < S; ++z) s += part[(size_t)z * n + i];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+// Column sums of an [P][C] tensor in a fixed order: stage 1 per (pixel slice, column), stage 2 over slices.
+constexpr int CS_SLICE = 1024;
+__global__ void colsum_partial_kernel(const float* __restrict__ x, int64_t P, int C, float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int64_t p0 = (int64_t)blockIdx.y * CS_SLICE;
+  const int64_t p1 = p0 + CS_SLICE < P ? p0 + CS_SLICE : P;
+  float s = 0.f;
+  for (int64_t p = p0; p < p1; ++p) s += x[p * C + c];
+  part[(int64_t)blockIdx.y * C + c] = s;
+}
+__global__ void colsum_final_kernel(const float* __restrict__ part, int S, int C, float* __restrict__ out,
+                                    int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int z = 0; z < S; ++z) s += part[(int64_t)z * C + c];
+  out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// GroupNorm(32) forward for training (code/nn.py:46-48, + scale/shift nn.py:203-206, + SiLU):
+//   stats[n][g] = (mean, rstd), rstd = 1/sqrt(var + 1e-5), biased var, accumulated in float64;
+//   out = act((x - mean) * rstd * gamma + beta) [ * (1 + scale) + shift ]
+// ss (optional): [N][ss_stride], scale at [0, C), shift at [C, 2C) (the emb projection's chunk order).
+constexpr int GN_SL = 256;  // pixels per partial block
+__global__ void gn_stat_partial_kernel(const float* __restrict__ x, int HW, int C, double* __restrict__ part) {
+  // grid (slices, N); thread = channel (C <= 1024 in steps of blockDim)
+  __shared__ double s1[1024], s2[1024];
+  const int n = blockIdx.y;
+  const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, HW);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double a = 0.0, b = 0.0;
+    for (int p = p0; p < p1; ++p) {
+      const double v = x[((int64_t)n * HW + p) * C + c];
+      a += v;
+      b += v * v;
+    }
+    s1[c] = a;
+    s2[c] = b;
+  }
+  __syncthreads();
+  const int cg = C / 32;
+  if (threadIdx.x < 32) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < cg; ++k) {
+      a += s1[threadIdx.x * cg + k];
+      b += s2[threadIdx.x * cg + k];
+    }
+    double* o = part + (((int64_t)n * gridDim.x + blockIdx.x) * 32 + threadIdx.x) * 2;
+    o[0] = a;
+    o[1] = b;
+  }
+}
+__global__ void gn_stat_final_kernel(const double* __restrict__ part, int nsl, int HW, int C, int N,
+                                     float* __restrict__ stats) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (n, g)
+  if (i >= N * 32) return;
+  const int n = i / 32, g = i % 32;
+  double a = 0.0, b = 0.0;
+  for (int s = 0; s < nsl; ++s) {
+    a += part[(((int64_t)n * nsl + s) * 32 + g) * 2];
+    b += part[(((int64_t)n * nsl + s) * 32 + g) * 2 + 1];
+  }
+  const double cnt = (double)HW * (C / 32);
+  const double mean = a / cnt;
+  double var = b / cnt - mean * mean;
+  if (var < 0) var = 0;
+  stats[i * 2] = (float)mean;
+  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+}
+
+__device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + expf(-z)); }
+
+__global__ void gn_apply_kernel(const float* __restrict__ x, int64_t tot, int HW, int C, const float* __restrict__ stats,
+                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                const float* __restrict__ ss, int ss_stride, int act_silu, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int c = (int)(i % C);
+  const int64_t pix = i / C;
+  const int n = (int)(pix / HW);
+  const int g = c / (C / 32);
+  const float mean = stats[(n * 32 + g) * 2], rstd = stats[(n * 32 + g) * 2 + 1];
+  float z = (x[i] - mean) * rstd * gamma[c] + beta[c];
+  if (ss) z = z * (1.0f + ss[(int64_t)n * ss_stride + c]) + ss[(int64_t)n * ss_stride + C + c];
+  out[i] = act_silu ? z * sigm(z) : z;
+}
+
+// GroupNorm(+ scale/shift)(+ SiLU) backward. With xhat = (x - mean) rstd, nrm = xhat gamma + beta,
+// z = nrm (1 + s) + sh (or nrm), a = silu(z) (or z), given da:
+//   dz = da silu'(z); dnrm = dz (1 + s); dsh = sum_p dz; ds = sum_p dz nrm;
+//   dgamma = sum dnrm xhat; dbeta = sum dnrm; dxhat = dnrm gamma;
+//   dx = rstd (dxhat - mean_g(dxhat) - xhat mean_g(dxhat xhat))
+// Pass 1 (per image n, pixel slice, channel): A1 = sum dz, A2 = sum dz nrm, A3 = sum dnrm xhat.
+struct GnBwdArgs {
+  const float* dout; const float* x; int N, HW, C;
+  const float* gamma; const float* beta; const float* ss; int ss_stride; int act_silu;
+  const float* stats;
+};
+__device__ __forceinline__ void gn_bwd_point(const GnBwdArgs& a, int n, int c, float xv, float dav, float& xhat,
+                                             float& nrm, float& dz, float& onep) {
+  const int g = c / (a.C / 32);
+  const float mean = a.stats[(n * 32 + g) * 2], rstd = a.stats[(n * 32 + g) * 2 + 1];
+  xhat = (xv - mean) * rstd;
+  nrm = xhat * a.gamma[c] + a.beta[c];
+  float z = nrm;
+  onep = 1.0f;
+  if (a.ss) {
+    onep = 1.0f + a.ss[(int64_t)n * a.ss_stride + c];
+    z = nrm * onep + a.ss[(int64_t)n * a.ss_stride + a.C + c];
+  }
+  if (a.act_silu) {
+    const float sg = sigm(z);
+    dz = dav * (sg * (1.0f + z * (1.0f - sg)));
+  } else {
+    dz = dav;
+  }
+}
+__global__ void gn_bwd_partial_kernel(GnBwdArgs a, float* __restrict__ part) {
+  // grid (slices, N); part [N][nsl][C][3]
+  const int n = blockIdx.y;
+  const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, a.HW);
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (int p = p0; p < p1; ++p) {
+      const int64_t i = ((int64_t)n * a.HW + p) * a.C + c;
+      float xhat, nrm, dz, onep;
+      gn_bwd_point(a, n, c, a.x[i], a.dout[i], xhat, nrm, dz, onep);
+      s1 += dz;
+      s2 += dz * nrm;
+      s3 += dz * onep * xhat;
+    }
+    float* o = part + (((int64_t)n * gridDim.x + blockIdx.x) * a.C + c) * 3;
+    o[0] = s1;
+    o[1] = s2;
+    o[2] = s3;
+  }
+}
+// per (n, c): A1..A3 (float64 over slices) -> dss, and per-(n, g) means -> red[n][g][2]
+__global__ void gn_bwd_reduce_kernel(GnBwdArgs a, const float* __restrict__ part, int nsl, float* __restrict__ nc,
+                                     float* __restrict__ dss) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (n, c)
+  if (i >= a.N * a.C) return;
+  const int n = i / a.C, c = i % a.C;
+  double s1 = 0, s2 = 0, s3 = 0;
+  for (int s = 0; s < nsl; ++s) {
+    const float* o = part + (((int64_t)n * nsl + s) * a.C + c) * 3;
+    s1 += o[0];
+    s2 += o[1];
+    s3 += o[2];
+  }
+  const float onep = a.ss ? 1.0f + a.ss[(int64_t)n * a.ss_stride + c] : 1.0f;
+  nc[i * 3] = (float)s1;           // sum dz
+  nc[i * 3 + 1] = (float)(s1 * onep);  // sum dnrm
+  nc[i * 3 + 2] = (float)s3;       // sum dnrm xhat
+  if (dss) {  // d scale, d shift (accumulated into the emb-projection gradient)
+    dss[(int64_t)n * a.ss_stride + c] += (float)s2;
+    dss[(int64_t)n * a.ss_stride + a.C + c] += (float)s1;
+  }
+}
+__global__ void gn_bwd_group_kernel(GnBwdArgs a, const float* __restrict__ nc, float* __restrict__ red) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (n, g)
+  if (i >= a.N * 32) return;
+  const int n = i / 32, g = i % 32, cg = a.C / 32;
+  double m1 = 0, m2 = 0;
+  for (int k = 0; k < cg; ++k) {
+    const int c = g * cg + k;
+    m1 += (double)a.gamma[c] * nc[((int64_t)n * a.C + c) * 3 + 1];
+    m2 += (double)a.gamma[c] * nc[((int64_t)n * a.C + c) * 3 + 2];
+  }
+  const double cnt = (double)cg * a.HW;
+  red[i * 2] = (float)(m1 / cnt);
+  red[i * 2 + 1] = (float)(m2 / cnt);
+}
+__global__ void gn_bwd_param_kernel(GnBwdArgs a, const float* __restrict__ nc, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  double g = 0, b = 0;
+  for (int n = 0; n < a.N; ++n) {
+    b += nc[((int64_t)n * a.C + c) * 3 + 1];
+    g += nc[((int64_t)n * a.C + c) * 3 + 2];
+  }
+  dgamma[c] += (float)g;
+  dbeta[c] += (float)b;
+}
+__global__ void gn_bwd_dx_kernel(GnBwdArgs a, const float* __restrict__ red, float* __restrict__ dx, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)a.N * a.HW * a.C;
+  if (i >= tot) return;
+  const int c = (int)(i % a.C);
+  const int n = (int)(i / ((int64_t)a.HW * a.C));
+  float xhat, nrm, dz, onep;
+  gn_bwd_point(a, n, c, a.x[i], a.dout[i], xhat, nrm, dz, onep);
+  const int g = c / (a.C / 32);
+  const float rstd = a.stats[(n * 32 + g) * 2 + 1];
+  const float dxhat = dz * onep * a.gamma[c];
+  const float v = rstd * (dxhat - red[(n * 32 + g) * 2] - xhat * red[(n * 32 + g) * 2 + 1]);
+  dx[i] = accumulate ? dx[i] + v : v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// nearest-up x2 / avg-pool 2x2 (code/nn.py:92-133) and their adjoints, NHWC.
+__global__ void resample_kernel(const float* __restrict__ x, int N, int Hin, int C, int mode, float* __restrict__ out) {
+  const int Ho = mode == 1 ? 2 * Hin : Hin / 2;
+  const int64_t tot = (int64_t)N * Ho * Ho * C;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int c = (int)(i % C);
+  int64_t r = i / C;
+  const int xo = (int)(r % Ho);
+  r /= Ho;
+  const int yo = (int)(r % Ho);
+  const int n = (int)(r / Ho);
+  if (mode == 1) {
+    out[i] = x[(((int64_t)n * Hin + yo / 2) * Hin + xo / 2) * C + c];
+  } else {
+    const int64_t b0 = (((int64_t)n * Hin + 2 * yo) * Hin + 2 * xo) * C + c;
+    const int64_t rs = (int64_t)Hin * C;
+    float s = x[b0];
+    s = s + x[b0 + C];
+    s = s + x[b0 + rs];
+    s = s + x[b0 + rs + C];
+    out[i] = s / 4.0f;
+  }
+}
+// dx at the input resolution from dy at the output resolution
+__global__ void resample_bwd_kernel(const float* __restrict__ dy, int N, int Hin, int C, int mode,
+                                    float* __restrict__ dx, int accumulate) {
+  const int64_t tot = (int64_t)N * Hin * Hin * C;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int c = (int)(i % C);
+  int64_t r = i / C;
+  const int x = (int)(r % Hin);
+  r /= Hin;
+  const int y = (int)(r % Hin);
+  const int n = (int)(r / Hin);
+  float v;
+  if (mode == 1) {  // up: each input pixel feeds a 2x2 block
+    const int Ho = 2 * Hin;
+    const int64_t b0 = (((int64_t)n * Ho + 2 * y) * Ho + 2 * x) * C + c;
+    const int64_t rs = (int64_t)Ho * C;
+    v = ((dy[b0] + dy[b0 + C]) + dy[b0 + rs]) + dy[b0 + rs + C];
+  } else {  // down: each input pixel gets a quarter of its pooled output's gradient
+    const int Ho = Hin / 2;
+    v = dy[(((int64_t)n * Ho + y / 2) * Ho + x / 2) * C + c] / 4.0f;
+  }
+  dx[i] = accumulate ? dx[i] + v : v;
+}
+
+__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+// dst[p][doff + c] (+)= src[p][soff + c], c < nc: concat assembly and the split of its gradient
+__global__ void copy_channels_kernel(const float* __restrict__ src, int cs, int soff, float* __restrict__ dst, int cd,
+                                     int doff, int nc, int64_t npix, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix * nc) return;
+  const int64_t p = i / nc;
+  const int c = (int)(i % nc);
+  const float v = src[p * cs + soff + c];
+  float* d = dst + p * cd + doff + c;
+  *d = accumulate ? *d + v : v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// QKVAttention backward (code/nn.py:222-235, chunk-first heads). Per (n, head): q, k, v [T][64]
+// at channel offsets (0, C, 2C) + 64 head of the qkv row; s2 = scale^2; P = softmax(s2 q k^T),
+// o = P v. Given do: dv = P^T do; dP = do v^T; dS = P (dP - rowsum(dP P)); dq = s2 dS k; dk = s2 dS^T q.
+// Kernel A: one block per (n, head, 32 query rows): recompute P rows, dP, dS; write dq and the
+// P / dS rows to scratch [N][H][T][T]. Kernel B: one block per (n, head, 32 key rows): dk, dv.
+constexpr int AB_R = 32;
+__global__ __launch_bounds__(256) void attn_bwd_rows_kernel(const float* __restrict__ qkv, const float* __restrict__ dout,
+                                                            int T, int C, float scale, float* __restrict__ dqkv,
+                                                            float* __restrict__ Pm, float* __restrict__ dSm) {
+  extern __shared__ float sh[];
+  float* S = sh;                    // [AB_R][T]
+  float* dP = sh + AB_R * T;        // [AB_R][T]
+  const int head = blockIdx.y, n = blockIdx.z, nh = gridDim.y;
+  const int r0 = blockIdx.x * AB_R;
+  const int64_t row = 3 * (int64_t)C;
+  const float* base = qkv + (int64_t)n * T * row;
+  const float* dob = dout + (int64_t)n * T * C;
+  const int qo = head * 64, ko = C + head * 64, vo = 2 * C + head * 64;
+  const float s2 = scale * scale;
+  for (int e = threadIdx.x; e < AB_R * T; e += blockDim.x) {
+    const int r = e / T, s = e % T, tq = r0 + r;
+    float acc = 0.f, accp = 0.f;
+    if (tq < T) {
+      for (int d = 0; d < 64; ++d) {
+        acc += (base[tq * row + qo + d] * scale) * (base[(int64_t)s * row + ko + d] * scale);
+        accp += dob[(int64_t)tq * C + head * 64 + d] * base[(int64_t)s * row + vo + d];
+      }
+    }
+    S[e] = acc;
+    dP[e] = accp;
+  }
+  __syncthreads();
+  // softmax rows (fp32, max-subtracted), then dS
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int r = wave; r < AB_R; r += 4) {
+    if (r0 + r >= T) continue;
+    float m = -INFINITY;
+    for (int s = lane; s < T; s += 64) m = fmaxf(m, S[r * T + s]);
+    for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float sum = 0.f;
+    for (int s = lane; s < T; s += 64) {
+      const float e = expf(S[r * T + s] - m);
+      S[r * T + s] = e;
+      sum += e;
+    }
+    for (int o = 32; o; o >>= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.0f / sum;
+    float dd = 0.f;
+    for (int s = lane; s < T; s += 64) {
+      const float p = S[r * T + s] * inv;
+      S[r * T + s] = p;
+      dd += dP[r * T + s] * p;
+    }
+    for (int o = 32; o; o >>= 1) dd += __shfl_xor(dd, o);
+    for (int s = lane; s < T; s += 64) dP[r * T + s] = S[r * T + s] * (dP[r * T + s] - dd);
+  }
+  __syncthreads();
+  const int64_t mo = (((int64_t)n * nh + head) * T + r0) * T;
+  for (int e = threadIdx.x; e < AB_R * T; e += blockDim.x) {
+    if (r0 + e / T < T) {
+      Pm[mo + e] = S[e];
+      dSm[mo + e] = dP[e];
+    }
+  }
+  // dq[tq][d] = s2 sum_s dS[tq][s] k[s][d]
+  for (int e = threadIdx.x; e < AB_R * 64; e += blockDim.x) {
+    const int r = e / 64, d = e % 64, tq = r0 + r;
+    if (tq >= T) continue;
+    float acc = 0.f;
+    for (int s = 0; s < T; ++s) acc += dP[r * T + s] * base[(int64_t)s * row + ko + d];
+    dqkv[((int64_t)n * T + tq) * row + qo + d] = s2 * acc;
+  }
+}
+__global__ __launch_bounds__(256) void attn_bwd_cols_kernel(const float* __restrict__ qkv, const float* __restrict__ dout,
+                                                            int T, int C, float scale, float* __restrict__ dqkv,
+                                                            const float* __restrict__ Pm, const float* __restrict__ dSm) {
+  const int head = blockIdx.y, n = blockIdx.z, nh = gridDim.y;
+  const int s0 = blockIdx.x * AB_R;
+  const int64_t row = 3 * (int64_t)C;
+  const float* base = qkv + (int64_t)n * T * row;
+  const float* dob = dout + (int64_t)n * T * C;
+  const int qo = head * 64, ko = C + head * 64, vo = 2 * C + head * 64;
+  const float s2 = scale * scale;
+  const int64_t mo = ((int64_t)n * nh + head) * T * T;
+  for (int e = threadIdx.x; e < AB_R * 64; e += blockDim.x) {
+    const int r = e / 64, d = e % 64, s = s0 + r;
+    if (s >= T) continue;
+    float dk = 0.f, dv = 0.f;
+    for (int t = 0; t < T; ++t) {
+      dk += dSm[mo + (int64_t)t * T + s] * base[(int64_t)t * row + qo + d];
+      dv += Pm[mo + (int64_t)t * T + s] * dob[(int64_t)t * C + head * 64 + d];
+    }
+    dqkv[((int64_t)n * T + s) * row + ko + d] = s2 * dk;
+    dqkv[((int64_t)n * T + s) * row + vo + d] = dv;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Linear layers of the embedding path (code/unet.py:44-48, code/nn.py:167-170): y = pre(x) W^T + b,
+// W [N][K] (torch), pre = identity | SiLU. M (the batch) is small; one thread per output.
+__device__ __forceinline__ float pre_f(float v, int pre_silu) { return pre_silu ? v * sigm(v) : v; }
+__global__ void linear_kernel(const float* __restrict__ x, int M, int K, const float* __restrict__ w,
+                              const float* __restrict__ b, int N, int pre_silu, int post_silu, float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * N) return;
+  const int m = (int)(i / N), j = (int)(i % N);
+  float acc = 0.f;
+  for (int k = 0; k < K; ++k) acc = fmaf(pre_f(x[(int64_t)m * K + k], pre_silu), w[(int64_t)j * K + k], acc);
+  float v = acc + (b ? b[j] : 0.f);
+  y[i] = post_silu ? v * sigm(v) : v;
+}
+// dx[m][k] (+)= (sum_j dy[m][j] W[j][k]) * pre'(x[m][k])
+__global__ void linear_dx_kernel(const float* __restrict__ dy, const float* __restrict__ x, int M, int K,
+                                 const float* __restrict__ w, int N, int pre_silu, float* __restrict__ dx, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)M * K) return;
+  const int m = (int)(i / K), k = (int)(i % K);
+  float acc = 0.f;
+  for (int j = 0; j < N; ++j) acc = fmaf(dy[(int64_t)m * N + j], w[(int64_t)j * K + k], acc);
+  if (pre_silu) {
+    const float v = x[i], sg = sigm(v);
+    acc *= sg * (1.0f + v * (1.0f - sg));
+  }
+  dx[i] = accumulate ? dx[i] + acc : acc;
+}
+// dW[j][k] += sum_m dy[m][j] pre(x[m][k]); db[j] += sum_m dy[m][j]
+__global__ void linear_dw_kernel(const float* __restrict__ dy, const float* __restrict__ x, int M, int K, int N,
+                                 int pre_silu, float* __restrict__ dw, float* __restrict__ db) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * K) return;
+  const int j = (int)(i / K), k = (int)(i % K);
+  float acc = 0.f, accb = 0.f;
+  for (int m = 0; m < M; ++m) {
+    const float g = dy[(int64_t)m * N + j];
+    acc = fmaf(g, pre_f(x[(int64_t)m * K + k], pre_silu), acc);
+    accb += g;
+  }
+  dw[i] += acc;
+  if (db && k == 0) db[j] += accb;
+}
+// y = silu'(z) * dy for the time-MLP's hidden layer (z stored pre-activation)
+__global__ void silu_bwd_kernel(const float* __restrict__ z, const float* __restrict__ dy, float* __restrict__ dz,
+                                int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = z[i], sg = sigm(v);
+  dz[i] = dy[i] * (sg * (1.0f + v * (1.0f - sg)));
+}
+// timestep_embedding(t, dim) (code/nn.py:51-61): [cos(t f) | sin(t f)] with the fp32 frequency
+// table f (computed on the host exactly as the reference does)
+__global__ void temb_kernel(const int64_t* __restrict__ t, const float* __restrict__ freqs, int N, int dim,
+                            float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * dim) return;
+  const int n = i / dim, k = i % dim, half = dim / 2;
+  const int j = k < half ? k : k - half;
+  const float arg = (float)t[n] * freqs[j];
+  out[i] = k < half ? cosf(arg) : sinf(arg);
+}
+
+// ---------------------------------------------------------------------------------------------
+// training_losses (code/gaussian_diffusion.py:540-614), fused elementwise parts.
+// x_t = q_sample(x0, t, noise) (:172-189); injection (:114-157 via :572-582, injection_schedule
+// "all", cumulative noise): x_t = keep q_sample(x0, t[0], cached) + (1 - keep) x_t, keep = 1 - mask.
+// Coefficients come from fp32 tables (_extract_into_tensor gathers float64, then .float()).
+__global__ void q_sample_inject_kernel(const float* __restrict__ x0, const float* __restrict__ noise,
+                                       const float* __restrict__ cached, const float* __restrict__ mask,
+                                       const int64_t* __restrict__ t, const float* __restrict__ sa,
+                                       const float* __restrict__ s1m, int N, int HW, int inject,
+                                       float* __restrict__ xt) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * 3 * HW) return;
+  const int n = (int)(i / (3 * (int64_t)HW));
+  const int64_t p = i % HW;
+  const int64_t tn = t[n];
+  float v = sa[tn] * x0[i] + s1m[tn] * noise[i];
+  if (inject) {
+    const int64_t t0 = t[0];
+    const float w = sa[t0] * x0[i] + s1m[t0] * cached[i];
+    const float keep = 1.0f - mask[(int64_t)n * HW + p];
+    v = keep * w + (1.0f - keep) * v;
+  }
+  xt[i] = v;
+}
+// masked eps-MSE: per (n, c): S = sum_p (noise - eps)^2 mask, area = max(sum_p mask, 1);
+// loss = mean over (n, c) of S / area; d eps = -2 (noise - eps) mask / area / (N * 3), written
+// into the NHWC gradient of the 6-channel model output (variance channels: 0).
+__global__ void mse_partial_kernel(const float* __restrict__ out6, int cs, const float* __restrict__ noise,
+                                   const float* __restrict__ mask, int HW, float* __restrict__ part) {
+  // grid (N * 3); block reduces over HW
+  __shared__ double r1[256], r2[256];
+  const int nc = blockIdx.x, n = nc / 3, c = nc % 3;
+  double a = 0.0, b = 0.0;
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    const float m = mask[(int64_t)n * HW + p];
+    const float d = noise[((int64_t)n * 3 + c) * HW + p] - out6[((int64_t)n * HW + p) * cs + c];
+    a += (double)(d * d * m);
+    b += m;
+  }
+  r1[threadIdx.x] = a;
+  r2[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s; s >>= 1) {
+    if (threadIdx.x < s) {
+      r1[threadIdx.x] += r1[threadIdx.x + s];
+      r2[threadIdx.x] += r2[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[nc * 2] = (float)r1[0];
+    part[nc * 2 + 1] = (float)(r2[0] < 1.0 ? 1.0 : r2[0]);
+  }
+}
+__global__ void mse_final_kernel(const float* __restrict__ part, int NC, float* __restrict__ loss) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < NC; ++i) s += (double)part[i * 2] / part[i * 2 + 1];
+  loss[0] = (float)(s / NC);
+}
+__global__ void mse_grad_kernel(const float* __restrict__ out6, int cs, const float* __restrict__ noise,
+                                const float* __restrict__ mask, const float* __restrict__ part, int N, int HW,
+                                float* __restrict__ dout6) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * HW * cs) return;
+  const int c = (int)(i % cs);
+  const int64_t pix = i / cs;
+  const int n = (int)(pix / HW);
+  const int64_t p = pix % HW;
+  float g = 0.f;
+  if (c < 3) {
+    const float m = mask[(int64_t)n * HW + p];
+    const float d = noise[((int64_t)n * 3 + c) * HW + p] - out6[i];
+    g = -2.0f * d * m / part[(n * 3 + c) * 2 + 1] / (float)(N * 3);
+  }
+  dout6[i] = g;
+}
+
+// ---------------------------------------------------------------------------------------------
+// clip_grad_norm_(max_norm) + AdamW (code/train_inpainting.py:64-66, :394-399; torch semantics):
+//   coef = min(1, max_norm / (||g|| + 1e-6)); g *= coef
+//   p *= 1 - lr wd; m = b1 m + (1 - b1) g; v = b2 v + (1 - b2) g^2
+//   p -= (lr / (1 - b1^k)) m / (sqrt(v) / sqrt(1 - b2^k) + eps)
+constexpr int SQ_BLOCKS = 1024;
+__global__ void sumsq_partial_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ part) {
+  __shared__ double r[256];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = g[i];
+    s += v * v;
+  }
+  r[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k; k >>= 1) {
+    if (threadIdx.x < k) r[threadIdx.x] += r[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = r[0];
+}
+__global__ void clip_coef_kernel(const double* __restrict__ part, int nb, float max_norm, float* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < nb; ++i) s += part[i];
+  const float norm = (float)sqrt(s);
+  const float coef = max_norm / (norm + 1e-6f);
+  out[0] = norm;
+  out[1] = coef < 1.0f ? coef : 1.0f;
+}
+__global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                             int64_t n, const float* __restrict__ clip, float lr, float b1, float b2, float eps,
+                             float wd, float bc1, float bc2s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i] * clip[1];
+  g[i] = gi;
+  float pi = p[i] * (1.0f - lr * wd);
+  const float mi = m[i] + (gi - m[i]) * (1.0f - b1);  // torch lerp_
+  const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2s + eps;
+  pi = pi - (lr / bc1) * (mi / denom);
+  p[i] = pi;
+}
+
+}  // namespace
+}  // namespace ifd
+
+using namespace ifd;
+
+#define TR_LAST() ((int)hipGetLastError())
+
+extern "C" {
+
+int ifd_tr_pack_conv(const float* w, int cout, int cin, int taps, int bn, int cin_pad, int cout_pad, int transpose,
+                     float* wpack, void* stream) {
+  const int64_t tot = (int64_t)cout_pad * cin_pad * taps;
+  if (!w || !wpack || cin_pad % 8 || cout_pad % bn || (taps != 1 && taps != 9)) {
+    set_error("ifd_tr_pack_conv: bad arguments");
+    return 2;
+  }
+  hipLaunchKernelGGL(pack_conv_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, w, cout, cin, taps, bn,
+                     cin_pad, cout_pad, transpose, wpack);
+  return TR_LAST();
+}
+
+static void conv_params(ConvParams& p, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                        const float* wpack, const float* bias, int cin_pad, int cout, int cout_pad, int bn, int taps,
+                        const float* res, float* out) {
+  std::memset(&p, 0, sizeof(p));
+  p.in0 = x0; p.c0 = c0; p.in1 = x1; p.c1 = c1;
+  p.N = N; p.Hin = p.Win = p.H = p.W = H;
+  p.act = ACT_NONE;
+  p.wpack = wpack; p.bias = bias;
+  p.cin_pad = cin_pad; p.cout = cout; p.cout_pad = cout_pad;
+  p.res = res; p.res_xform = XF_NONE; p.res_H = p.res_W = H;
+  p.out = out;
+  p.epi = EPI_NHWC;
+  conv_geometry(p, H, H, N, bn, cin_pad / 8);
+}
+
+int64_t ifd_tr_conv_part_floats(int N, int H, int cin_pad, int cout, int cout_pad, int bn) {
+  ConvParams p;
+  conv_params(p, nullptr, cin_pad, nullptr, 0, N, H, nullptr, nullptr, cin_pad, cout, cout_pad, bn, 9, nullptr,
+              nullptr);
+  return p.ksplit > 1 ? (int64_t)p.ksplit * N * H * H * cout : 0;
+}
+
+int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* wpack, const float* bias,
+                int cin_pad, int cout, int cout_pad, int bn, int taps, const float* res, float* out, float* part,
+                int64_t part_floats, void* stream) {
+  // cout % 4: the NHWC epilogue stores channel quads
+  if ((H & (H - 1)) || c0 % 8 || c1 % 8 || c0 + c1 != cin_pad || (bn != 32 && bn != 64) || cout_pad % bn ||
+      cout % 4 || cout > cout_pad || (taps != 1 && taps != 9) || !x0 || !out || !wpack || !bias) {
+    set_error("ifd_tr_conv: unsupported arguments");
+    return 2;
+  }
+  ConvParams p;
+  conv_params(p, x0, c0, c1 ? x1 : nullptr, c1, N, H, wpack, bias, cin_pad, cout, cout_pad, bn, taps, res, out);
+  if (p.ksplit > 1) {
+    if (!part || (int64_t)p.ksplit * N * H * H * cout > part_floats) {
+      set_error("ifd_tr_conv: split-K workspace too small (ifd_tr_conv_part_floats)");
+      return 2;
+    }
+    p.part = part;
+  }
+  int e = launch_conv(p, taps, XF_NONE, bn, (hipStream_t)stream);
+  if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, (hipStream_t)stream);
+  if (e) set_error(std::string("ifd_tr_conv: ") + hipGetErrorString((hipError_t)e));
+  return e;
+}
+
+int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* splits) {
+  const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64) * taps;
+  const int64_t nch = (P + WG_CH - 1) / WG_CH;
+  int S = 1;
+  while (S < 256 && (int64_t)tiles * S < 1024 && nch / (2 * S) >= 8) S *= 2;
+  if (splits) *splits = S;
+  return (int64_t)S * cout * cin * taps;
+}
+
+int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                      int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
+                      int64_t colpart_floats, void* stream) {
+  const int cin = c0 + c1;
+  const int64_t P = (int64_t)N * H * H;
+  int S = 1;
+  const int64_t need = ifd_tr_wgrad_part_floats(cout, cin, taps, P, &S);
+  if (!dy || !x0 || !dw || !part || need > part_floats || c0 % 4 || (taps != 1 && taps != 9)) {
+    set_error("ifd_tr_conv_wgrad: bad arguments or workspace too small");
+    return 2;
+  }
+  WgArgs a;
+  a.dy = dy; a.cout = cout; a.x0 = x0; a.c0 = c0; a.x1 = c1 ? x1 : x0; a.c1 = c1;
+  a.N = N; a.H = H; a.W = H; a.taps = taps; a.P = P;
+  const int64_t nch = (P + WG_CH - 1) / WG_CH;
+  a.chunks_per_split = (int)((nch + S - 1) / S);
+  a.part = part;
+  const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64) * taps;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, S), dim3(256), 0, s, a);
+  const int64_t n = (int64_t)cout * cin * taps;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
+  if (db) {
+    const int slices = (int)((P + CS_SLICE - 1) / CS_SLICE);
+    if (!colpart || (int64_t)slices * cout > colpart_floats) {
+      set_error("ifd_tr_conv_wgrad: column-sum workspace too small");
+      return 2;
+    }
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((cout + 63) / 64, slices), dim3(64), 0, s, dy, P, cout, colpart);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((cout + 63) / 64), dim3(64), 0, s, colpart, slices, cout, db, 1);
+  }
+  return TR_LAST();
+}
+
+int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
+                  int ss_stride, int act_silu, float* out, float* stats, double* work, int64_t work_doubles,
+                  void* stream) {
+  const int nsl = (HW + GN_SL - 1) / GN_SL;
+  if (C % 32 || C > 1024 || (int64_t)N * nsl * 64 > work_doubles) {
+    set_error("ifd_tr_gn_fwd: C must be a multiple of 32 (<= 1024), work >= N * ceil(HW/256) * 64 doubles");
+    return 2;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gn_stat_partial_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, work);
+  hipLaunchKernelGGL(gn_stat_final_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, work, nsl, HW, C, N, stats);
+  const int64_t tot = (int64_t)N * HW * C;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid1(tot)), dim3(TB), 0, s, x, tot, HW, C, stats, gamma, beta, ss,
+                     ss_stride, act_silu, out);
+  return TR_LAST();
+}
+
+int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
+                  const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
+                  float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream) {
+  const int nsl = (HW + GN_SL - 1) / GN_SL;
+  const int64_t need = (int64_t)N * nsl * C * 3 + (int64_t)N * C * 3 + (int64_t)N * 64;
+  if (C % 32 || need > work_floats) {
+    set_error("ifd_tr_gn_bwd: C must be a multiple of 32; work too small");
+    return 2;
+  }
+  GnBwdArgs a{dout, x, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats};
+  float* part = work;
+  float* nc = work + (int64_t)N * nsl * C * 3;
+  float* red = nc + (int64_t)N * C * 3;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gn_bwd_partial_kernel, dim3(nsl, N), dim3(256), 0, s, a, part);
+  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(grid1(N * C)), dim3(TB), 0, s, a, part, nsl, nc, dss);
+  hipLaunchKernelGGL(gn_bwd_group_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, a, nc, red);
+  hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
+  const int64_t tot = (int64_t)N * HW * C;
+  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(grid1(tot)), dim3(TB), 0, s, a, red, dx, accumulate);
+  return TR_LAST();
+}
+
+int ifd_tr_resample(const float* x, int N, int Hin, int C, int mode, float* out, void* stream) {
+  if (mode != 1 && mode != 2) { set_error("ifd_tr_resample: mode 1 (up) or 2 (down)"); return 2; }
+  const int Ho = mode == 1 ? 2 * Hin : Hin / 2;
+  const int64_t tot = (int64_t)N * Ho * Ho * C;
+  hipLaunchKernelGGL(resample_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, x, N, Hin, C, mode, out);
+  return TR_LAST();
+}
+
+int ifd_tr_resample_bwd(const float* dy, int N, int Hin, int C, int mode, float* dx, int accumulate, void* stream) {
+  if (mode != 1 && mode != 2) { set_error("ifd_tr_resample_bwd: mode 1 (up) or 2 (down)"); return 2; }
+  const int64_t tot = (int64_t)N * Hin * Hin * C;
+  hipLaunchKernelGGL(resample_bwd_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, dy, N, Hin, C, mode, dx,
+                     accumulate);
+  return TR_LAST();
+}
+
+int ifd_tr_add(const float* a, const float* b, float* out, int64_t n, void* stream) {
+  hipLaunchKernelGGL(add_kernel, dim3(grid1(n)), dim3(TB), 0, (hipStream_t)stream, a, b, out, n);
+  return TR_LAST();
+}
+
+int ifd_tr_copy_channels(const float* src, int cs, int soff, float* dst, int cd, int doff, int nc, int64_t npix,
+                         int accumulate, void* stream) {
+  if (soff + nc > cs || doff + nc > cd) { set_error("ifd_tr_copy_channels: channel range"); return 2; }
+  hipLaunchKernelGGL(copy_channels_kernel, dim3(grid1(npix * nc)), dim3(TB), 0, (hipStream_t)stream, src, cs, soff, dst,
+                     cd, doff, nc, npix, accumulate);
+  return TR_LAST();
+}
+
+int ifd_tr_attention(const float* qkv, int N, int T, int C, float scale, float* out, void* stream) {
+  if (C % 64) { set_error("ifd_tr_attention: 64-channel heads"); return 2; }
+  launch_attention(qkv, N, T, C, scale, out, (hipStream_t)stream);
+  return TR_LAST();
+}
+
+int64_t ifd_tr_attention_bwd_scratch_floats(int N, int T, int C) { return 2 * (int64_t)N * (C / 64) * T * T; }
+
+int ifd_tr_attention_bwd(const float* qkv, const float* dout, int N, int T, int C, float scale, float* dqkv,
+                         float* scratch, int64_t scratch_floats, void* stream) {
+  const int nh = C / 64;
+  if (C % 64 || T > 1024 || ifd_tr_attention_bwd_scratch_floats(N, T, C) > scratch_floats) {
+    set_error("ifd_tr_attention_bwd: bad arguments or scratch too small");
+    return 2;
+  }
+  float* Pm = scratch;
+  float* dS = scratch + (int64_t)N * nh * T * T;
+  dim3 g((T + AB_R - 1) / AB_R, nh, N);
+  const size_t lds = (size_t)2 * AB_R * T * sizeof(float);
+  static bool attr[kMaxDevices] = {};
+  (void)set_lds_attr_once(attr, reinterpret_cast<const void*>(&attn_bwd_rows_kernel), (int)lds);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(attn_bwd_rows_kernel, g, dim3(256), lds, s, qkv, dout, T, C, scale, dqkv, Pm, dS);
+  hipLaunchKernelGGL(attn_bwd_cols_kernel, g, dim3(256), 0, s, qkv, dout, T, C, scale, dqkv, Pm, dS);
+  return TR_LAST();
+}
+
+int ifd_tr_linear(const float* x, int M, int K, const float* w, const float* b, int N, int pre_silu, int post_silu,
+                  float* y, void* stream) {
+  hipLaunchKernelGGL(linear_kernel, dim3(grid1((int64_t)M * N)), dim3(TB), 0, (hipStream_t)stream, x, M, K, w, b, N,
+                     pre_silu, post_silu, y);
+  return TR_LAST();
+}
+
+int ifd_tr_linear_bwd(const float* dy, const float* x, int M, int K, const float* w, int N, int pre_silu, float* dx,
+                      int dx_accumulate, float* dw, float* db, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dx)
+    hipLaunchKernelGGL(linear_dx_kernel, dim3(grid1((int64_t)M * K)), dim3(TB), 0, s, dy, x, M, K, w, N, pre_silu, dx,
+                       dx_accumulate);
+  if (dw)
+    hipLaunchKernelGGL(linear_dw_kernel, dim3(grid1((int64_t)N * K)), dim3(TB), 0, s, dy, x, M, K, N, pre_silu, dw, db);
+  return TR_LAST();
+}
+
+int ifd_tr_silu_bwd(const float* z, const float* dy, float* dz, int64_t n, void* stream) {
+  hipLaunchKernelGGL(silu_bwd_kernel, dim3(grid1(n)), dim3(TB), 0, (hipStream_t)stream, z, dy, dz, n);
+  return TR_LAST();
+}
+
+int ifd_tr_temb(const int64_t* t, const float* freqs, int N, int dim, float* out, void* stream) {
+  hipLaunchKernelGGL(temb_kernel, dim3(grid1(N * dim)), dim3(TB), 0, (hipStream_t)stream, t, freqs, N, dim, out);
+  return TR_LAST();
+}
+
+int ifd_tr_pack_input(const float* x, const float* masked_image, const float* mask, int N, int HW, float* out16,
+                      void* stream) {
+  launch_pack_input(x, masked_image, mask, 0, N, HW, out16, (hipStream_t)stream);
+  return TR_LAST();
+}
+
+int ifd_tr_q_sample_inject(const float* x0, const float* noise, const float* cached, const float* mask,
+                           const int64_t* t, const float* sqrt_ac, const float* sqrt_1m_ac, int N, int HW, int inject,
+                           float* xt, void* stream) {
+  const int64_t tot = (int64_t)N * 3 * HW;
+  hipLaunchKernelGGL(q_sample_inject_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, x0, noise, cached,
+                     mask, t, sqrt_ac, sqrt_1m_ac, N, HW, inject, xt);
+  return TR_LAST();
+}
+
+int ifd_tr_masked_mse(const float* out6_nhwc, int cs, const float* noise, const float* mask, int N, int HW,
+                      float* loss, float* dout6_nhwc, float* work, void* stream) {
+  if (cs < 3) { set_error("ifd_tr_masked_mse: channel stride < 3"); return 2; }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(mse_partial_kernel, dim3(N * 3), dim3(256), 0, s, out6_nhwc, cs, noise, mask, HW, work);
+  hipLaunchKernelGGL(mse_final_kernel, dim3(1), dim3(64), 0, s, work, N * 3, loss);
+  if (dout6_nhwc)
+    hipLaunchKernelGGL(mse_grad_kernel, dim3(grid1((int64_t)N * HW * cs)), dim3(TB), 0, s, out6_nhwc, cs, noise, mask,
+                       work, N, HW, dout6_nhwc);
+  return TR_LAST();
+}
+
+int ifd_tr_clip_adamw(float* p, float* g, float* m, float* v, int64_t n, float max_norm, float lr, float b1, float b2,
+                      float eps, float wd, int step, double* work, float* norm_coef, void* stream) {
+  if (step < 1 || !work || !norm_coef) { set_error("ifd_tr_clip_adamw: bad arguments"); return 2; }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(SQ_BLOCKS), dim3(256), 0, s, g, n, work);
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, s, work, SQ_BLOCKS, max_norm, norm_coef);
+  const float bc1 = 1.0f - (float)std::pow((double)b1, step);
+  const float bc2s = (float)std::sqrt(1.0 - std::pow((double)b2, step));
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid1(n)), dim3(TB), 0, s, p, g, m, v, n, norm_coef, lr, b1, b2, eps, wd, bc1,
+                     bc2s);
+  return TR_LAST();
+}
+
+}  // extern "C"

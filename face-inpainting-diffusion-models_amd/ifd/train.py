@@ -1,0 +1,508 @@
+"""Training step of the 9-channel inpainting UNet on the HIP library (BASELINE C5).
+
+One iteration of the reference's `train_epoch` (code/train_inpainting.py:15-79):
+
+    losses = diffusion.training_losses(model, images, t, {'masked_image', 'mask'})  (gaussian_diffusion.py:540-614)
+    losses['loss'].backward()
+    clip_grad_norm_(model.parameters(), 1.0)
+    AdamW(lr, weight_decay, betas=(0.9, 0.999)).step()
+
+runs here as `UNetTrainer.train_step`, every tensor operation a libifd kernel (include/ifd_train.h):
+q_sample + the known-region injection with the t[0]-keyed, never-cleared GT-noise cache, the UNet
+forward in fp32 keeping what the backward needs, the masked eps-MSE and its gradient, the
+backward of every module (conv dgrad / wgrad on fp32 MFMA, GroupNorm + scale/shift + SiLU,
+up/down-sampling, QKV attention, the embedding MLPs), the global grad-norm clip and a fused AdamW.
+PyTorch provides device memory and the stream only; nothing here computes through ATen.
+
+Parameters, gradients and both AdamW moments are four flat fp32 device buffers in the reference's
+state_dict order and torch layouts (`state_dict()` returns views with the reference's key names,
+`base_model.` prefixed like DiffusionInpaintingModel's). Activations are NHWC.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .topology import FULL, UNetConfig, layer_plan, state_dict_spec
+
+_c = ctypes
+vp, i32, i64, f32 = _c.c_void_p, _c.c_int, _c.c_int64, _c.c_float
+TRAIN_EXPORTS = {
+    "ifd_tr_pack_conv": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+    "ifd_tr_conv_part_floats": (i64, [i32, i32, i32, i32, i32, i32]),
+    "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
+    "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
+    "ifd_tr_conv_wgrad": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp]),
+    "ifd_tr_gn_fwd": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp, i64, vp]),
+    "ifd_tr_gn_bwd": (i32, [vp, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, i64, vp]),
+    "ifd_tr_resample": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+    "ifd_tr_resample_bwd": (i32, [vp, i32, i32, i32, i32, vp, i32, vp]),
+    "ifd_tr_add": (i32, [vp, vp, vp, i64, vp]),
+    "ifd_tr_copy_channels": (i32, [vp, i32, i32, vp, i32, i32, i32, i64, i32, vp]),
+    "ifd_tr_attention": (i32, [vp, i32, i32, i32, f32, vp, vp]),
+    "ifd_tr_attention_bwd_scratch_floats": (i64, [i32, i32, i32]),
+    "ifd_tr_attention_bwd": (i32, [vp, vp, i32, i32, i32, f32, vp, vp, i64, vp]),
+    "ifd_tr_linear": (i32, [vp, i32, i32, vp, vp, i32, i32, i32, vp, vp]),
+    "ifd_tr_linear_bwd": (i32, [vp, vp, i32, i32, vp, i32, i32, vp, i32, vp, vp, vp]),
+    "ifd_tr_silu_bwd": (i32, [vp, vp, vp, i64, vp]),
+    "ifd_tr_temb": (i32, [vp, vp, i32, i32, vp, vp]),
+    "ifd_tr_pack_input": (i32, [vp, vp, vp, i32, i32, vp, vp]),
+    "ifd_tr_q_sample_inject": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "ifd_tr_masked_mse": (i32, [vp, i32, vp, vp, i32, i32, vp, vp, vp, vp]),
+    "ifd_tr_clip_adamw": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, i32, vp, vp, vp]),
+}
+
+_bound = None
+
+
+def lib():
+    global _bound
+    L = _lib.lib()
+    if _bound is not L:
+        for name, (res, args) in TRAIN_EXPORTS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _bound = L
+    return L
+
+
+def P(t):
+    return None if t is None else _c.c_void_p(t.data_ptr())
+
+
+def chk(rc):
+    _lib.check(rc)
+
+
+def _bn(cout):
+    return 64 if cout % 64 == 0 else 32
+
+
+def _pad(v, m):
+    return (v + m - 1) // m * m
+
+
+class UNetTrainer:
+    """fp32 training of the 9-channel UNet (code/unet.py:14-200) with the reference's loss, clip and AdamW."""
+
+    def __init__(self, cfg: UNetConfig = FULL, device="cuda", lr=5e-5, weight_decay=0.01, betas=(0.9, 0.999),
+                 eps=1e-8, max_norm=1.0):
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        self.lr, self.wd, self.betas, self.eps, self.max_norm = lr, weight_decay, betas, eps, max_norm
+        self.spec = state_dict_spec(cfg, prefix="")
+        self.offsets = {}
+        n = 0
+        for k, shape in self.spec:
+            self.offsets[k] = (n, tuple(shape))
+            n += int(np.prod(shape))
+        self.numel = n
+        z = lambda: torch.zeros(n, device=self.dev, dtype=torch.float32)  # noqa: E731
+        self.flat, self.grad, self.m, self.v = z(), z(), z(), z()
+        self.step_count = 0
+        self.norm_coef = torch.zeros(2, device=self.dev)
+        self.loss = torch.zeros(1, device=self.dev)
+        self._gt_noise_cache = {}
+        # timestep_embedding frequencies exactly as the reference builds them (code/nn.py:54-56)
+        half = cfg.model_channels // 2
+        self.freqs = torch.exp(-math.log(10000) * torch.arange(0, half, dtype=torch.float32) / half).to(self.dev)
+        self._zero_bias = torch.zeros(4096, device=self.dev)
+        self.plan = layer_plan(cfg)
+        self.emb_dim = 4 * cfg.model_channels
+        self.s = None  # stream pointer (set per call)
+
+    # ------------------------------------------------------------------ parameters
+    def p(self, name):
+        o, shape = self.offsets[name]
+        return self.flat[o:o + int(np.prod(shape))].view(shape)
+
+    def g(self, name):
+        o, shape = self.offsets[name]
+        return self.grad[o:o + int(np.prod(shape))].view(shape)
+
+    def load_state_dict(self, sd):
+        sd = {(k[len("base_model."):] if k.startswith("base_model.") else k): v for k, v in sd.items()}
+        missing = [k for k, _ in self.spec if k not in sd]
+        if missing:
+            raise KeyError(f"missing parameters: {missing[:4]}...")
+        with torch.no_grad():
+            for k, _ in self.spec:
+                self.p(k).copy_(sd[k].to(self.dev, torch.float32))
+
+    def state_dict(self, prefix="base_model."):
+        return {prefix + k: self.p(k) for k, _ in self.spec}
+
+    def grads(self, prefix="base_model."):
+        return {prefix + k: self.g(k) for k, _ in self.spec}
+
+    # ------------------------------------------------------------------ op wrappers
+    def _empty(self, *shape):
+        return torch.empty(*shape, device=self.dev, dtype=torch.float32)
+
+    def _zeros(self, *shape):
+        return torch.zeros(*shape, device=self.dev, dtype=torch.float32)
+
+    def _packed(self, name, transpose):
+        """Device packing of conv weight `name` for the forward (transpose 0) or dgrad (1) conv."""
+        w = self.p(name)
+        cout, cin = w.shape[0], w.shape[1]
+        taps = int(np.prod(w.shape[2:])) if w.dim() > 2 else 1
+        pout, pin = (cout, cin) if not transpose else (cin, cout)
+        bn = _bn(pout)
+        cin_pad, cout_pad = _pad(pin, 8), _pad(pout, bn)
+        key = (name, transpose)
+        buf = self._pack_cache.get(key)
+        if buf is None:
+            buf = self._empty(cout_pad * cin_pad * taps)
+            chk(lib().ifd_tr_pack_conv(P(w), cout, cin, taps, bn, cin_pad, cout_pad, transpose, P(buf), self.s))
+            self._pack_cache[key] = buf
+        return buf, pout, pin, taps, bn, cin_pad, cout_pad
+
+    def conv(self, x, cin_x, N, H, name, bias_name=None, res=None, x1=None, c1=0, transpose=False):
+        """NHWC conv of concat(x[cin_x], x1[c1]) with weight `name` (forward or, transposed, dgrad).
+        Output channels are padded to a multiple of 4 (zero weight rows): the 6-channel head writes 8."""
+        buf, pout, pin, taps, bn, cin_pad, cout_pad = self._packed(name, int(transpose))
+        if cin_x + c1 != cin_pad:
+            raise ValueError(f"{name}: input channels {cin_x}+{c1} != packed {cin_pad}")
+        real = pout
+        pout = _pad(pout, 4)
+        out = self._empty(N, H, H, pout)
+        b = self.p(bias_name) if bias_name else self._zero_bias
+        if bias_name and real != pout:
+            b = self._zeros(pout)
+            b[:real].copy_(self.p(bias_name))
+        pf = lib().ifd_tr_conv_part_floats(N, H, cin_pad, pout, cout_pad, bn)
+        part = self._empty(max(pf, 1))
+        chk(lib().ifd_tr_conv(P(x), cin_x, P(x1), c1, N, H, P(buf), P(b), cin_pad, pout, cout_pad, bn, taps, P(res),
+                              P(out), P(part), pf, self.s))
+        return out
+
+    def wgrad(self, dy, cout, x, cin_x, N, H, name, bias_name=None, real_cin=None):
+        """grad[name] += conv weight gradient; grad[bias] += column sums of dy."""
+        w = self.p(name)
+        taps = int(np.prod(w.shape[2:])) if w.dim() > 2 else 1
+        P_ = N * H * H
+        S = _c.c_int()
+        need = lib().ifd_tr_wgrad_part_floats(cout, cin_x, taps, P_, _c.byref(S))
+        part = self._empty(need)
+        colpart = self._empty(((P_ + 1023) // 1024) * cout)
+        real_cin = real_cin or w.shape[1]
+        real_cout = w.shape[0]
+        direct = real_cin == cin_x and real_cout == cout
+        dw = self.g(name) if direct else self._zeros(cout * cin_x * taps)
+        db = self.g(bias_name) if (bias_name and real_cout == cout) else (self._zeros(cout) if bias_name else None)
+        chk(lib().ifd_tr_conv_wgrad(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
+                                    P(colpart), colpart.numel(), self.s))
+        if not direct:  # padded input (the first conv reads 16 channels, 9 real) or output (head: 8, 6 real)
+            chk(lib().ifd_tr_copy_channels(P(dw), cin_x * taps, 0, P(self.g(name)), real_cin * taps, 0, real_cin * taps,
+                                           real_cout, 1, self.s))
+        if bias_name and real_cout != cout:
+            chk(lib().ifd_tr_copy_channels(P(db), cout, 0, P(self.g(bias_name)), real_cout, 0, real_cout, 1, 1, self.s))
+
+    def gn_fwd(self, x, N, HW, C, prefix, ss=None, ss_stride=0, silu=True):
+        out = self._empty(N * HW * C)
+        stats = self._empty(N * 64)
+        nsl = (HW + 255) // 256
+        work = torch.empty(N * nsl * 64, device=self.dev, dtype=torch.float64)
+        chk(lib().ifd_tr_gn_fwd(P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")), P(ss),
+                                ss_stride, int(silu), P(out), P(stats), P(work), work.numel(), self.s))
+        return out, stats
+
+    def gn_bwd(self, dout, x, N, HW, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None, silu=True):
+        acc = dx is not None
+        if dx is None:
+            dx = self._empty(N * HW * C)
+        nsl = (HW + 255) // 256
+        work = self._empty(N * nsl * C * 3 + N * C * 3 + N * 64)
+        chk(lib().ifd_tr_gn_bwd(P(dout), P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")),
+                                P(ss), ss_stride, int(silu), P(stats), P(dx), int(acc), P(self.g(prefix + "weight")),
+                                P(self.g(prefix + "bias")), P(dss), P(work), work.numel(), self.s))
+        return dx
+
+    def resample(self, x, N, Hin, C, mode):
+        Ho = 2 * Hin if mode == 1 else Hin // 2
+        out = self._empty(N, Ho, Ho, C)
+        chk(lib().ifd_tr_resample(P(x), N, Hin, C, mode, P(out), self.s))
+        return out
+
+    def resample_bwd(self, dy, N, Hin, C, mode, dx=None):
+        acc = dx is not None
+        if dx is None:
+            dx = self._empty(N, Hin, Hin, C)
+        chk(lib().ifd_tr_resample_bwd(P(dy), N, Hin, C, mode, P(dx), int(acc), self.s))
+        return dx
+
+    def add_(self, dst, src):
+        chk(lib().ifd_tr_add(P(dst), P(src), P(dst), dst.numel(), self.s))
+        return dst
+
+    def copy_ch(self, src, cs, soff, dst, cd, doff, nc, npix, acc):
+        chk(lib().ifd_tr_copy_channels(P(src), cs, soff, P(dst), cd, doff, nc, npix, int(acc), self.s))
+
+    def linear(self, x, M, name_w, name_b, pre_silu=False):
+        w = self.p(name_w)
+        y = self._empty(M, w.shape[0])
+        chk(lib().ifd_tr_linear(P(x), M, w.shape[1], P(w), P(self.p(name_b)), w.shape[0], int(pre_silu), 0, P(y), self.s))
+        return y
+
+    def linear_bwd(self, dy, x, M, name_w, name_b, pre_silu=False, dx=None, want_dx=True):
+        w = self.p(name_w)
+        acc = dx is not None
+        if want_dx and dx is None:
+            dx = self._empty(M, w.shape[1])
+        chk(lib().ifd_tr_linear_bwd(P(dy), P(x), M, w.shape[1], P(w), w.shape[0], int(pre_silu),
+                                    P(dx) if want_dx else None, int(acc), P(self.g(name_w)), P(self.g(name_b)), self.s))
+        return dx
+
+    # ------------------------------------------------------------------ forward / backward
+    def forward(self, x, t, masked_image, mask):
+        """UNet forward (code/unet.py:154-173, 197-200) keeping the activations the backward needs.
+        x, masked_image [N,3,H,W], mask [N,1,H,W] NCHW fp32; t int64 [N]. Returns out6 NHWC [N,H,W,6]."""
+        cfg = self.cfg
+        N, _, H, _ = x.shape
+        self._pack_cache = {}
+        self.s = _lib.stream_ptr(self.dev)
+        tape = {"N": N, "H": H}
+        # time embedding: temb -> Linear -> SiLU -> Linear (unet.py:44-48); all emb_layers (nn.py:167-170)
+        temb = self._empty(N, cfg.model_channels)
+        chk(lib().ifd_tr_temb(P(t), P(self.freqs), N, cfg.model_channels, P(temb), self.s))
+        z0 = self.linear(temb, N, "time_embed.0.weight", "time_embed.0.bias")
+        emb = self.linear(z0, N, "time_embed.2.weight", "time_embed.2.bias", pre_silu=True)
+        tape.update(temb=temb, z0=z0, emb=emb, E={})
+        x16 = self._empty(N, H, H, 16)
+        chk(lib().ifd_tr_pack_input(P(x), P(masked_image), P(mask), N, H * H, P(x16), self.s))
+        tape["x16"] = x16
+        hs, saved = [], {}
+        h, hc, hr = None, 0, H
+        for section, bi, layers in self.plan:
+            if section == "output":
+                skip = hs.pop()
+                sc = skip.shape[-1]
+                cat = self._empty(N, hr, hr, hc + sc)
+                self.copy_ch(h, hc, 0, cat, hc + sc, 0, hc, N * hr * hr, False)
+                self.copy_ch(skip, sc, 0, cat, hc + sc, hc, sc, N * hr * hr, False)
+                h, hc = cat, hc + sc
+            for L in layers:
+                k, p = L["kind"], L["prefix"]
+                if k == "conv_in":
+                    h = self.conv(x16, 16, N, hr, p + "weight", p + "bias")
+                    hc = L["cout"]
+                elif k in ("res", "res_down", "res_up"):
+                    h, hr = self._res_fwd(L, h, N, hr, emb, saved)
+                    hc = L["cout"]
+                elif k == "attn":
+                    h = self._attn_fwd(L, h, N, hr, saved)
+                elif k == "out":
+                    a, st = self.gn_fwd(h, N, hr * hr, hc, "out.0.", silu=True)
+                    saved["out"] = dict(x=h, a=a, stats=st)
+                    h = self.conv(a, hc, N, hr, "out.2.weight", "out.2.bias")
+                    hc = L["cout"]
+            if section == "input":
+                hs.append(h)
+        tape["saved"] = saved
+        self._tape = tape
+        return h  # [N, H, W, 8]: the 6 output channels, then 2 zero channels
+
+    def _res_fwd(self, L, x, N, r, emb, saved):
+        """ResBlock._forward (code/nn.py:189-212), scale-shift norm, resblock_updown."""
+        p, cin, cout, k = L["prefix"], L["cin"], L["cout"], L["kind"]
+        a1, st1 = self.gn_fwd(x, N, r * r, cin, p + "in_layers.0.", silu=True)
+        mode = 1 if k == "res_up" else (2 if k == "res_down" else 0)
+        ro = 2 * r if mode == 1 else (r // 2 if mode == 2 else r)
+        a1r = self.resample(a1, N, r, cin, mode) if mode else a1
+        xr = self.resample(x, N, r, cin, mode) if mode else x
+        h1 = self.conv(a1r, cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
+        E = self.linear(emb, N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True)  # [N, 2 cout]
+        a2, st2 = self.gn_fwd(h1, N, ro * ro, cout, p + "out_layers.0.", ss=E, ss_stride=2 * cout, silu=True)
+        if cin != cout:
+            skip = self.conv(xr, cin, N, ro, p + "skip_connection.weight", p + "skip_connection.bias")
+        else:
+            skip = xr
+        out = self.conv(a2, cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias", res=skip)
+        saved[p] = dict(x=x, a1r=a1r, xr=xr, h1=h1, a2=a2, E=E, st1=st1, st2=st2, mode=mode, r=r, ro=ro)
+        return out, ro
+
+    def _attn_fwd(self, L, x, N, r, saved):
+        """AttentionBlock._forward (code/nn.py:259-265) with QKVAttention (:222-235)."""
+        p, C = L["prefix"], L["cin"]
+        T = r * r
+        n, st = self.gn_fwd(x, N, T, C, p + "norm.", silu=False)
+        qkv = self.conv(n, C, N, r, p + "qkv.weight", p + "qkv.bias")
+        a = self._empty(N, T, C)
+        scale = 1.0 / math.sqrt(math.sqrt(self.cfg.num_head_channels))
+        chk(lib().ifd_tr_attention(P(qkv), N, T, C, scale, P(a), self.s))
+        out = self.conv(a, C, N, r, p + "proj_out.weight", p + "proj_out.bias", res=x)
+        saved[p] = dict(x=x, n=n, st=st, qkv=qkv, a=a, scale=scale)
+        return out
+
+    def backward(self, dout6):
+        """Gradients of every parameter (+= into the flat grad buffer) from d loss / d out6 (NHWC)."""
+        tape = self._tape
+        N, H = tape["N"], tape["H"]
+        saved = tape["saved"]
+        emb = tape["emb"]
+        demb = self._zeros(N, self.emb_dim)
+        # output head: conv 128 -> 6 (its dgrad input padded to 8 channels)
+        so = saved["out"]
+        hc = so["x"].shape[-1]
+        co = dout6.shape[-1]  # the head's channel count padded to 4 (zero gradient in the pad)
+        self.wgrad(dout6, co, so["a"], hc, N, H, "out.2.weight", "out.2.bias")
+        da = self.conv(dout6, co, N, H, "out.2.weight", transpose=True)
+        dh = self.gn_bwd(da, so["x"], N, H * H, hc, "out.0.", so["stats"], silu=True)
+        # hs gradients from the output blocks' skip inputs
+        in_blocks = [b for b in self.plan if b[0] == "input"]
+        dhs = [None] * len(in_blocks)
+        hs_idx = 0  # the last output block (first here) consumed hs[0]
+        r = H
+        for section, bi, layers in reversed(self.plan):
+            if section in ("out",):
+                continue
+            if section == "input":
+                break
+            for L in reversed(layers):
+                dh, r = self._layer_bwd(L, dh, N, saved, demb)
+            if section == "output":
+                # split d cat(h, skip) (code/unet.py:170)
+                cin = layers[0]["cin"]
+                sc = layers[0]["skip_ch"]
+                hcur = cin - sc
+                dprev = self._empty(N, r, r, hcur)
+                self.copy_ch(dh, cin, 0, dprev, hcur, 0, hcur, N * r * r, False)
+                ds_ = self._empty(N, r, r, sc)
+                self.copy_ch(dh, cin, hcur, ds_, sc, 0, sc, N * r * r, False)
+                dhs[hs_idx] = ds_
+                hs_idx += 1
+                dh = dprev
+        # middle block's input = the last input block's output: dh continues down the input chain
+        for bidx in range(len(in_blocks) - 1, -1, -1):
+            section, bi, layers = in_blocks[bidx]
+            self.add_(dh, dhs[bidx])
+            for L in reversed(layers):
+                if L["kind"] == "conv_in":
+                    self.wgrad(dh, L["cout"], tape["x16"], 16, N, r, L["prefix"] + "weight", L["prefix"] + "bias",
+                               real_cin=L["cin"])
+                    dh = None
+                else:
+                    dh, r = self._layer_bwd(L, dh, N, saved, demb)
+        # embedding MLP backward (unet.py:44-48)
+        dz0 = self.linear_bwd(demb, tape["z0"], N, "time_embed.2.weight", "time_embed.2.bias", pre_silu=True)
+        self.linear_bwd(dz0, tape["temb"], N, "time_embed.0.weight", "time_embed.0.bias", want_dx=False)
+
+    def _layer_bwd(self, L, dout, N, saved, demb):
+        k, p = L["kind"], L["prefix"]
+        if k == "attn":
+            sv = saved[p]
+            C = L["cin"]
+            r = int(round(math.sqrt(sv["a"].shape[1])))
+            T = r * r
+            self.wgrad(dout, C, sv["a"], C, N, r, p + "proj_out.weight", p + "proj_out.bias")
+            da = self.conv(dout, C, N, r, p + "proj_out.weight", transpose=True)
+            dqkv = self._empty(N, T, 3 * C)
+            sf = lib().ifd_tr_attention_bwd_scratch_floats(N, T, C)
+            scratch = self._empty(sf)
+            chk(lib().ifd_tr_attention_bwd(P(sv["qkv"]), P(da), N, T, C, sv["scale"], P(dqkv), P(scratch), sf, self.s))
+            self.wgrad(dqkv, 3 * C, sv["n"], C, N, r, p + "qkv.weight", p + "qkv.bias")
+            dn = self.conv(dqkv, 3 * C, N, r, p + "qkv.weight", transpose=True)
+            dx = self.gn_bwd(dn, sv["x"], N, T, C, p + "norm.", sv["st"], silu=False)
+            self.add_(dx, dout)
+            return dx, r
+        sv = saved[p]
+        cin, cout, mode, r, ro = L["cin"], L["cout"], sv["mode"], sv["r"], sv["ro"]
+        # h2 = conv2(a2) + b2; out = skip + h2
+        self.wgrad(dout, cout, sv["a2"], cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias")
+        da2 = self.conv(dout, cout, N, ro, p + "out_layers.3.weight", transpose=True)
+        dE = self._zeros(N, 2 * cout)
+        dh1 = self.gn_bwd(da2, sv["h1"], N, ro * ro, cout, p + "out_layers.0.", sv["st2"], ss=sv["E"],
+                          ss_stride=2 * cout, dss=dE, silu=True)
+        self.linear_bwd(dE, self._tape["emb"], N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True,
+                        dx=demb)
+        self.wgrad(dh1, cout, sv["a1r"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
+        da1r = self.conv(dh1, cout, N, ro, p + "in_layers.2.weight", transpose=True)
+        da1 = self.resample_bwd(da1r, N, r, cin, mode) if mode else da1r
+        dx = self.gn_bwd(da1, sv["x"], N, r * r, cin, p + "in_layers.0.", sv["st1"], silu=True)
+        if cin != cout:
+            self.wgrad(dout, cout, sv["xr"], cin, N, ro, p + "skip_connection.weight", p + "skip_connection.bias")
+            dxr = self.conv(dout, cout, N, ro, p + "skip_connection.weight", transpose=True)
+        else:
+            dxr = dout
+        if mode:
+            self.resample_bwd(dxr, N, r, cin, mode, dx=dx)
+        else:
+            self.add_(dx, dxr)
+        return dx, r
+
+    # ------------------------------------------------------------------ loss / step
+    def tables(self, diffusion):
+        key = id(diffusion)
+        if getattr(self, "_tables_key", None) != key:
+            self._sa = torch.from_numpy(diffusion.sqrt_alphas_cumprod).float().to(self.dev)
+            self._s1m = torch.from_numpy(diffusion.sqrt_one_minus_alphas_cumprod).float().to(self.dev)
+            self._tables_key = key
+        return self._sa, self._s1m
+
+    def training_loss(self, diffusion, x_start, t, model_kwargs, noise=None, use_injection=True, noise_device=None):
+        """GaussianDiffusion.training_losses (code/gaussian_diffusion.py:540-614) for the MSE loss with
+        LEARNED_RANGE output, injection schedule "all" and cumulative GT noise: returns the loss (device
+        scalar) and keeps d loss / d out6 for `backward`. RNG draws in the reference's order: noise (if not
+        given), then the GT-noise cache entry for (shape, t[0]) on first use; the cache is never cleared."""
+        self.s = _lib.stream_ptr(self.dev)
+        N, _, H, W = x_start.shape
+        mask = model_kwargs.get("mask")
+        masked = model_kwargs.get("masked_image")
+        if mask is None:
+            mask = torch.ones(N, 1, H, W, device=self.dev)
+        if noise is None:
+            noise = (torch.randn(x_start.shape, device=noise_device) if noise_device else
+                     torch.randn_like(x_start)).to(self.dev)
+        inject = bool(use_injection and masked is not None)
+        cached = noise
+        if inject:
+            t0 = int(t[0].item())  # the reference's int(t[0].item()) (gaussian_diffusion.py:131)
+            key = (tuple(x_start.shape), t0)
+            cached = self._gt_noise_cache.get(key)
+            if cached is None:
+                cached = (torch.randn(x_start.shape, device=noise_device) if noise_device else
+                          torch.randn_like(x_start)).to(self.dev)
+                self._gt_noise_cache[key] = cached
+        sa, s1m = self.tables(diffusion)
+        xt = self._empty(N, 3, H, W)
+        x0c, nc_, mc = (v.to(self.dev, torch.float32).contiguous() for v in (x_start, noise, mask))
+        tt = t.to(self.dev, torch.int64).contiguous()
+        chk(lib().ifd_tr_q_sample_inject(P(x0c), P(nc_), P(cached.contiguous()), P(mc), P(tt), P(sa), P(s1m), N,
+                                         H * W, int(inject), P(xt), self.s))
+        mi = masked.to(self.dev, torch.float32).contiguous() if masked is not None else self._zeros(N, 3, H, W)
+        out6 = self.forward(xt, tt, mi, mc)  # [N, H, W, 8]: channels 0-5 the model output
+        cs = out6.shape[-1]
+        self._dout6 = self._empty(N, H, W, cs)
+        work = self._empty(N * 6)
+        chk(lib().ifd_tr_masked_mse(P(out6), cs, P(nc_), P(mc), N, H * W, P(self.loss), P(self._dout6), P(work),
+                                    self.s))
+        self._keep = (xt, mi, mc, nc_, x0c, tt)
+        return self.loss
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def optimizer_step(self):
+        """clip_grad_norm_(max_norm) + AdamW (code/train_inpainting.py:64-66); norm on device, no sync."""
+        self.step_count += 1
+        work = torch.empty(1024, device=self.dev, dtype=torch.float64)
+        b1, b2 = self.betas
+        chk(lib().ifd_tr_clip_adamw(P(self.flat), P(self.grad), P(self.m), P(self.v), self.numel, self.max_norm,
+                                    self.lr, b1, b2, self.eps, self.wd, self.step_count, P(work), P(self.norm_coef),
+                                    _lib.stream_ptr(self.dev)))
+
+    def train_step(self, diffusion, images, masked_images, masks, t, noise=None, noise_device=None):
+        """One iteration of train_epoch (code/train_inpainting.py:27-66): zero_grad, training_losses,
+        backward, clip_grad_norm_(1.0), AdamW.step(). Returns the loss as a device scalar."""
+        self.zero_grad()
+        loss = self.training_loss(diffusion, images, t, {"masked_image": masked_images, "mask": masks}, noise=noise,
+                                  noise_device=noise_device)
+        self.backward(self._dout6)
+        self.optimizer_step()
+        return loss

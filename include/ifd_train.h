@@ -1,0 +1,92 @@
+/* ifd training ops — the C ABI of the fp32 training step (BASELINE configs[4]).
+ *
+ * Replaces, for the 9-channel UNet of code/unet.py / code/nn.py, what the reference's
+ * `train_epoch` (code/train_inpainting.py:15-79) gets from torch autograd + optim:
+ *   loss = diffusion.training_losses(model, x_start, t, model_kwargs)['loss']
+ *                                        (code/gaussian_diffusion.py:540-614)
+ *   loss.backward()                      (code/train_inpainting.py:61)
+ *   clip_grad_norm_(params, 1.0)         (:64)
+ *   AdamW(lr, wd, betas=(0.9, 0.999)).step()   (:66, :394-399)
+ * The host side (ifd/train.py) orchestrates these ops over the reference's module graph; every
+ * tensor argument is a DEVICE pointer, activations are NHWC fp32 [N][H][W][C], weights are in the
+ * reference's torch layouts ([Cout][Cin][kh][kw], Linear [out][in]). All launches are async on
+ * `stream`; reductions run in a fixed order (bit-reproducible). Status 0 = ok, else see
+ * ifd_last_error(). Accumulating outputs (dw, db, dgamma, dbeta, dss) are added into (+=).
+ */
+#ifndef IFD_TRAIN_H
+#define IFD_TRAIN_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* conv weight W[cout][cin][taps] -> the fp32 conv kernel's packing; transpose=1 packs the dgrad kernel
+ * (out channels = cin, in channels = cout, taps flipped). cin_pad / cout_pad / bn are the PACKED conv's
+ * (bn = 64 if its out count % 64 == 0 else 32; cin_pad a multiple of 8). */
+int ifd_tr_pack_conv(const float* w, int cout, int cin, int taps, int bn, int cin_pad, int cout_pad, int transpose,
+                     float* wpack, void* stream);
+/* out[N,H,H,cout] = conv(concat(x0[c0], x1[c1])) + bias (+ res): nn.Conv2d 3x3 pad 1 (taps 9) or 1x1
+ * (code/nn.py:12-20,184,252,254); cout % 4 == 0 (pad: weights packed with zero rows);
+ * split-K slabs in `part` (size: ifd_tr_conv_part_floats). */
+int64_t ifd_tr_conv_part_floats(int N, int H, int cin_pad, int cout, int cout_pad, int bn);
+int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* wpack, const float* bias,
+                int cin_pad, int cout, int cout_pad, int bn, int taps, const float* res, float* out, float* part,
+                int64_t part_floats, void* stream);
+/* dw[cout][c0+c1][taps] += sum_pixels dy (x) shifted concat(x0, x1); db[cout] += column sums of dy. */
+int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* splits);
+int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                      int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
+                      int64_t colpart_floats, void* stream);
+/* GroupNorm(32, C) (+ scale/shift: ss[n][0:C] = scale, ss[n][C:2C] = shift, row stride ss_stride) (+ SiLU).
+ * stats[n][32][2] = (mean, rstd) saved for the backward; work: N * ceil(HW/256) * 64 doubles. */
+int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
+                  int ss_stride, int act_silu, float* out, float* stats, double* work, int64_t work_doubles,
+                  void* stream);
+/* its backward: dx (= or +=), dgamma/dbeta +=, dss (d scale, d shift) +=.
+ * work: N*ceil(HW/256)*C*3 + N*C*3 + N*64 floats. */
+int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
+                  const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
+                  float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream);
+/* nearest-up x2 (mode 1) / AvgPool2d(2) (mode 2) (code/nn.py:92-133) and the adjoint (dx at Hin). */
+int ifd_tr_resample(const float* x, int N, int Hin, int C, int mode, float* out, void* stream);
+int ifd_tr_resample_bwd(const float* dy, int N, int Hin, int C, int mode, float* dx, int accumulate, void* stream);
+int ifd_tr_add(const float* a, const float* b, float* out, int64_t n, void* stream);
+/* dst[p][doff+c] (=|+=) src[p][soff+c], c < nc: the skip concat (code/unet.py:170) and its gradient split */
+int ifd_tr_copy_channels(const float* src, int cs, int soff, float* dst, int cd, int doff, int nc, int64_t npix,
+                         int accumulate, void* stream);
+/* QKVAttention (code/nn.py:222-235) on qkv [N][T][3C] -> out [N][T][C], and its backward (dqkv written). */
+int ifd_tr_attention(const float* qkv, int N, int T, int C, float scale, float* out, void* stream);
+int64_t ifd_tr_attention_bwd_scratch_floats(int N, int T, int C);
+int ifd_tr_attention_bwd(const float* qkv, const float* dout, int N, int T, int C, float scale, float* dqkv,
+                         float* scratch, int64_t scratch_floats, void* stream);
+/* y[M][N] = post(pre(x) W^T + b), W [N][K] (nn.Linear), pre/post SiLU optional; backward: dx (= or +=,
+ * times pre'(x)), dw +=, db +=. */
+int ifd_tr_linear(const float* x, int M, int K, const float* w, const float* b, int N, int pre_silu, int post_silu,
+                  float* y, void* stream);
+int ifd_tr_linear_bwd(const float* dy, const float* x, int M, int K, const float* w, int N, int pre_silu, float* dx,
+                      int dx_accumulate, float* dw, float* db, void* stream);
+int ifd_tr_silu_bwd(const float* z, const float* dy, float* dz, int64_t n, void* stream);
+/* timestep_embedding (code/nn.py:51-61) from an fp32 frequency table freqs[dim/2]. */
+int ifd_tr_temb(const int64_t* t, const float* freqs, int N, int dim, float* out, void* stream);
+/* the 9-channel input [x, masked_image, mask x3] (code/unet.py:199) as NHWC with 16 channels (7 zero). */
+int ifd_tr_pack_input(const float* x, const float* masked_image, const float* mask, int N, int HW, float* out16,
+                      void* stream);
+/* x_t = q_sample(x0, t, noise); inject: keep * q_sample(x0, t[0], cached) + (1 - keep) * x_t, keep = 1 - mask
+ * (code/gaussian_diffusion.py:566-582). sqrt_ac / sqrt_1m_ac: the fp32-rounded float64 tables. NCHW. */
+int ifd_tr_q_sample_inject(const float* x0, const float* noise, const float* cached, const float* mask,
+                           const int64_t* t, const float* sqrt_ac, const float* sqrt_1m_ac, int N, int HW, int inject,
+                           float* xt, void* stream);
+/* masked eps-MSE (code/gaussian_diffusion.py:595-610) on channels 0-2 of the model output (NHWC, channel
+ * stride cs >= 6): loss[0] and d loss / d out (same layout, other channels 0). work: 6N floats. */
+int ifd_tr_masked_mse(const float* out6_nhwc, int cs, const float* noise, const float* mask, int N, int HW,
+                      float* loss, float* dout6_nhwc, float* work, void* stream);
+/* clip_grad_norm_(max_norm) then AdamW over one flat parameter buffer; norm_coef[0] = grad norm,
+ * [1] = clip coefficient (device; no host sync). work: 1024 doubles. step >= 1. */
+int ifd_tr_clip_adamw(float* p, float* g, float* m, float* v, int64_t n, float max_norm, float lr, float b1, float b2,
+                      float eps, float wd, int step, double* work, float* norm_coef, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -53,3 +53,26 @@ def test_unknown_weight_name_is_an_error():
     buf = (ctypes.c_float * 3)()
     rc = _lib.lib().ifd_load_weights(h.h, b"nope.weight", ctypes.cast(buf, ctypes.c_void_p), shape, 1)
     assert rc != 0 and b"unexpected parameter" in _lib.lib().ifd_last_error()
+
+
+def test_library_exports_train_header_symbols():
+    """include/ifd_train.h (the training-step ops) is exported in full and bound by ifd.train."""
+    src = open(os.path.join(ROOT, "include", "ifd_train.h")).read()
+    syms = sorted(set(re.findall(r"\b(ifd_tr_[a-z_0-9]+)\s*\(", src)))
+    assert len(syms) >= 20
+    from ifd import train
+    L = train.lib()
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(train.TRAIN_EXPORTS)
+
+
+def test_train_host_helpers():
+    """Split-K / workspace size queries need no GPU: the wgrad split covers the chip for small layers."""
+    import ctypes as c
+    from ifd import train
+    L = train.lib()
+    S = c.c_int()
+    n = L.ifd_tr_wgrad_part_floats(128, 128, 9, 2 * 64 * 64, c.byref(S))
+    assert S.value >= 2 and n == S.value * 128 * 128 * 9
+    assert L.ifd_tr_attention_bwd_scratch_floats(2, 16, 128) == 2 * 2 * 2 * 16 * 16
