@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -109,6 +110,58 @@ def spawn_ranks(n):
     return subprocess.run(cmd, env=env).returncode
 
 
+def train_main(args):
+    """`--workload train`: BASELINE configs[4]'s training step (code/train_inpainting.py:15-79), fp32 as the
+    reference trains (no bf16 / LoRA exists in the reference), B images per GPU at 256x256: t ~ randint,
+    training_losses with injection, backward, clip_grad_norm_(1.0), AdamW. Step = one optimizer step.
+    Multi-GPU: per-rank steps (data parallelism would add an all-reduce of the 374 MB gradient; not part of
+    the reference, which trains on one device)."""
+    from ifd import parallel
+    from ifd.manifest import make_state_dict
+    from ifd.schedules import create_gaussian_diffusion
+    from ifd.topology import FULL, gflop_per_image
+    from ifd.train import UNetTrainer
+    rank, ws, local = parallel.world()
+    dev = parallel.device_for(local)
+    torch.cuda.set_device(dev)
+    parallel.init(device=dev)
+    B, H = args.batch, FULL.image_size
+    tr = UNetTrainer(FULL, device=dev)
+    tr.load_state_dict(make_state_dict(FULL, seed=1))
+    diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="quadratic")
+    gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
+    masked = gt * (1 - mask)
+    gen = torch.Generator(device=dev).manual_seed(1 + rank)
+
+    def step():
+        t = torch.randint(0, 1000, (B,), device=dev, generator=gen)
+        return tr.train_step(diff, gt, masked, mask, t)
+    for _ in range(args.warmup):
+        step()
+    parallel.barrier(dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    parallel.barrier(dev)
+    elapsed = parallel.max_over_ranks(time.perf_counter() - t0, dev)
+    lossv = float(loss)
+    assert math.isfinite(lossv)
+    value = B * ws * args.steps / elapsed
+    gf = gflop_per_image(FULL)
+    res = {"metric": "training step images/sec (fp32 fwd+bwd+clip+AdamW, 256x256 9-ch UNet)", "value": round(value, 4),
+           "unit": "images/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32", "data": "synthetic (gt~U(-1,1), rectangle masks, seeded weights)",
+           "config": {"workload": "train_inpainting.py train_epoch step (BASELINE configs[4], fp32: the reference has no "
+                                  "bf16/LoRA)", "global_batch": B * ws, "batch_per_gpu": B,
+                      "parallelism": f"{ws} independent ranks"},
+           "loss": lossv, "algorithmic_tflops": round(3 * gf * B * ws * args.steps / elapsed / 1e3, 2)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,12 +176,16 @@ def main():
                     help="conv arithmetic: the fp32-accurate 3xf16 split MFMA (default), or exact fp32 MFMA")
     ap.add_argument("--fp32-exact-steps", type=int, default=1,
                     help="N=1 only: also time this many steps in exact-fp32 mode (0 = skip)")
+    ap.add_argument("--workload", choices=["sample", "train"], default="sample",
+                    help="sample: the headline DDIM-100 sampler (default); train: the training step (configs[4])")
     ap.add_argument("--noise", choices=["device", "parity"], default="device",
                     help="device: per-rank GPU RNG (throughput); parity: full-batch host draws in reference order, "
                          "sliced per rank (GPU-count-independent results)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    if args.workload == "train":
+        return train_main(args)
 
     from ifd import parallel
     from ifd.manifest import make_state_dict

@@ -168,16 +168,28 @@ __global__ void slab_reduce_kernel(const float* __restrict__ part, int S, int64_
   out[i] = accumulate ? out[i] + s : s;
 }
 
-// Column sums of an [P][C] tensor in a fixed order: stage 1 per (pixel slice, column), stage 2 over slices.
-constexpr int CS_SLICE = 1024;
-__global__ void colsum_partial_kernel(const float* __restrict__ x, int64_t P, int C, float* __restrict__ part) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const int64_t p0 = (int64_t)blockIdx.y * CS_SLICE;
-  const int64_t p1 = p0 + CS_SLICE < P ? p0 + CS_SLICE : P;
+// Column sums of an [P][C] tensor in a fixed order: stage 1 per (pixel slice, column) — a block is
+// 64 columns x 4 row lanes (each row lane strides the slice's pixels, coalesced along the columns),
+// merged in LDS in lane order; stage 2 adds the slices in order (float64).
+constexpr int CS_SLICE = 1024;  // the smallest slice; large tensors use multiples (<= 256 slices)
+inline int64_t colsum_slice(int64_t P) {
+  int64_t sl = CS_SLICE;
+  while ((P + sl - 1) / sl > 256) sl *= 2;
+  return sl;
+}
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x, int64_t P, int C,
+                                                             int64_t slice, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int64_t p0 = (int64_t)blockIdx.y * slice;
+  const int64_t p1 = p0 + slice < P ? p0 + slice : P;
   float s = 0.f;
-  for (int64_t p = p0; p < p1; ++p) s += x[p * C + c];
-  part[(int64_t)blockIdx.y * C + c] = s;
+  if (c < C)
+    for (int64_t p = p0 + rl; p < p1; p += 4) s += x[p * C + c];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < C) part[(int64_t)blockIdx.y * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 __global__ void colsum_final_kernel(const float* __restrict__ part, int S, int C, float* __restrict__ out,
                                     int accumulate) {
@@ -538,24 +550,39 @@ __global__ __launch_bounds__(256) void attn_bwd_cols_kernel(const float* __restr
 // Linear layers of the embedding path (code/unet.py:44-48, code/nn.py:167-170): y = pre(x) W^T + b,
 // W [N][K] (torch), pre = identity | SiLU. M (the batch) is small; one thread per output.
 __device__ __forceinline__ float pre_f(float v, int pre_silu) { return pre_silu ? v * sigm(v) : v; }
-__global__ void linear_kernel(const float* __restrict__ x, int M, int K, const float* __restrict__ w,
-                              const float* __restrict__ b, int N, int pre_silu, int post_silu, float* __restrict__ y) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)M * N) return;
-  const int m = (int)(i / N), j = (int)(i % N);
+// one wave per (output column j, row m): lanes stride k (the weight row read coalesced), then a
+// fixed-order shuffle tree
+__global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ x, int M, int K,
+                                                     const float* __restrict__ w, const float* __restrict__ b, int N,
+                                                     int pre_silu, int post_silu, float* __restrict__ y) {
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wid >= (int64_t)M * N) return;
+  const int m = (int)(wid / N), j = (int)(wid % N);
   float acc = 0.f;
-  for (int k = 0; k < K; ++k) acc = fmaf(pre_f(x[(int64_t)m * K + k], pre_silu), w[(int64_t)j * K + k], acc);
-  float v = acc + (b ? b[j] : 0.f);
-  y[i] = post_silu ? v * sigm(v) : v;
+  for (int k = lane; k < K; k += 64) acc = fmaf(pre_f(x[(int64_t)m * K + k], pre_silu), w[(int64_t)j * K + k], acc);
+  for (int o = 32; o; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) {
+    const float v = acc + (b ? b[j] : 0.f);
+    y[wid] = post_silu ? v * sigm(v) : v;
+  }
 }
-// dx[m][k] (+)= (sum_j dy[m][j] W[j][k]) * pre'(x[m][k])
-__global__ void linear_dx_kernel(const float* __restrict__ dy, const float* __restrict__ x, int M, int K,
-                                 const float* __restrict__ w, int N, int pre_silu, float* __restrict__ dx, int accumulate) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)M * K) return;
-  const int m = (int)(i / K), k = (int)(i % K);
-  float acc = 0.f;
-  for (int j = 0; j < N; ++j) acc = fmaf(dy[(int64_t)m * N + j], w[(int64_t)j * K + k], acc);
+// dx[m][k] (+)= (sum_j dy[m][j] W[j][k]) * pre'(x[m][k]); block = 64 k x 4 j-quarters (merged in order)
+__global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                        int M, int K, const float* __restrict__ w, int N, int pre_silu,
+                                                        float* __restrict__ dx, int accumulate) {
+  __shared__ float red[4][64];
+  const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int kblocks = (K + 63) / 64;
+  const int m = blockIdx.x / kblocks, k = (blockIdx.x % kblocks) * 64 + kl;
+  float part = 0.f;
+  if (k < K)
+    for (int j = q; j < N; j += 4) part = fmaf(dy[(int64_t)m * N + j], w[(int64_t)j * K + k], part);
+  red[q][kl] = part;
+  __syncthreads();
+  if (q != 0 || k >= K) return;
+  const int64_t i = (int64_t)m * K + k;
+  float acc = ((red[0][kl] + red[1][kl]) + red[2][kl]) + red[3][kl];
   if (pre_silu) {
     const float v = x[i], sg = sigm(v);
     acc *= sg * (1.0f + v * (1.0f - sg));
@@ -756,12 +783,13 @@ static void conv_params(ConvParams& p, const float* x0, int c0, const float* x1,
   p.res = res; p.res_xform = XF_NONE; p.res_H = p.res_W = H;
   p.out = out;
   p.epi = EPI_NHWC;
+  p.opt_bm128 = taps == 1;  // the 256-pixel tiles are instantiated for 3x3 only
   conv_geometry(p, H, H, N, bn, cin_pad / 8);
 }
 
-int64_t ifd_tr_conv_part_floats(int N, int H, int cin_pad, int cout, int cout_pad, int bn) {
+int64_t ifd_tr_conv_part_floats(int N, int H, int cin_pad, int cout, int cout_pad, int bn, int taps) {
   ConvParams p;
-  conv_params(p, nullptr, cin_pad, nullptr, 0, N, H, nullptr, nullptr, cin_pad, cout, cout_pad, bn, 9, nullptr,
+  conv_params(p, nullptr, cin_pad, nullptr, 0, N, H, nullptr, nullptr, cin_pad, cout, cout_pad, bn, taps, nullptr,
               nullptr);
   return p.ksplit > 1 ? (int64_t)p.ksplit * N * H * H * cout : 0;
 }
@@ -822,12 +850,14 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
   const int64_t n = (int64_t)cout * cin * taps;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (db) {
-    const int slices = (int)((P + CS_SLICE - 1) / CS_SLICE);
+    const int64_t slice = colsum_slice(P);
+    const int slices = (int)((P + slice - 1) / slice);
     if (!colpart || (int64_t)slices * cout > colpart_floats) {
       set_error("ifd_tr_conv_wgrad: column-sum workspace too small");
       return 2;
     }
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3((cout + 63) / 64, slices), dim3(64), 0, s, dy, P, cout, colpart);
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((cout + 63) / 64, slices), dim3(256), 0, s, dy, P, cout, slice,
+                       colpart);
     hipLaunchKernelGGL(colsum_final_kernel, dim3((cout + 63) / 64), dim3(64), 0, s, colpart, slices, cout, db, 1);
   }
   return TR_LAST();
@@ -931,8 +961,8 @@ int ifd_tr_attention_bwd(const float* qkv, const float* dout, int N, int T, int 
 
 int ifd_tr_linear(const float* x, int M, int K, const float* w, const float* b, int N, int pre_silu, int post_silu,
                   float* y, void* stream) {
-  hipLaunchKernelGGL(linear_kernel, dim3(grid1((int64_t)M * N)), dim3(TB), 0, (hipStream_t)stream, x, M, K, w, b, N,
-                     pre_silu, post_silu, y);
+  hipLaunchKernelGGL(linear_kernel, dim3(grid1((int64_t)M * N * 64)), dim3(TB), 0, (hipStream_t)stream, x, M, K, w, b,
+                     N, pre_silu, post_silu, y);
   return TR_LAST();
 }
 
@@ -940,7 +970,7 @@ int ifd_tr_linear_bwd(const float* dy, const float* x, int M, int K, const float
                       int dx_accumulate, float* dw, float* db, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dx)
-    hipLaunchKernelGGL(linear_dx_kernel, dim3(grid1((int64_t)M * K)), dim3(TB), 0, s, dy, x, M, K, w, N, pre_silu, dx,
+    hipLaunchKernelGGL(linear_dx_kernel, dim3(M * ((K + 63) / 64)), dim3(256), 0, s, dy, x, M, K, w, N, pre_silu, dx,
                        dx_accumulate);
   if (dw)
     hipLaunchKernelGGL(linear_dw_kernel, dim3(grid1((int64_t)N * K)), dim3(TB), 0, s, dy, x, M, K, N, pre_silu, dw, db);

@@ -33,7 +33,7 @@ _c = ctypes
 vp, i32, i64, f32 = _c.c_void_p, _c.c_int, _c.c_int64, _c.c_float
 TRAIN_EXPORTS = {
     "ifd_tr_pack_conv": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
-    "ifd_tr_conv_part_floats": (i64, [i32, i32, i32, i32, i32, i32]),
+    "ifd_tr_conv_part_floats": (i64, [i32, i32, i32, i32, i32, i32, i32]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
     "ifd_tr_conv_wgrad": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp]),
@@ -176,7 +176,7 @@ class UNetTrainer:
         if bias_name and real != pout:
             b = self._zeros(pout)
             b[:real].copy_(self.p(bias_name))
-        pf = lib().ifd_tr_conv_part_floats(N, H, cin_pad, pout, cout_pad, bn)
+        pf = lib().ifd_tr_conv_part_floats(N, H, cin_pad, pout, cout_pad, bn, taps)
         part = self._empty(max(pf, 1))
         chk(lib().ifd_tr_conv(P(x), cin_x, P(x1), c1, N, H, P(buf), P(b), cin_pad, pout, cout_pad, bn, taps, P(res),
                               P(out), P(part), pf, self.s))

@@ -29,7 +29,7 @@ int ifd_tr_pack_conv(const float* w, int cout, int cin, int taps, int bn, int ci
 /* out[N,H,H,cout] = conv(concat(x0[c0], x1[c1])) + bias (+ res): nn.Conv2d 3x3 pad 1 (taps 9) or 1x1
  * (code/nn.py:12-20,184,252,254); cout % 4 == 0 (pad: weights packed with zero rows);
  * split-K slabs in `part` (size: ifd_tr_conv_part_floats). */
-int64_t ifd_tr_conv_part_floats(int N, int H, int cin_pad, int cout, int cout_pad, int bn);
+int64_t ifd_tr_conv_part_floats(int N, int H, int cin_pad, int cout, int cout_pad, int bn, int taps);
 int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* wpack, const float* bias,
                 int cin_pad, int cout, int cout_pad, int bn, int taps, const float* res, float* out, float* part,
                 int64_t part_floats, void* stream);
