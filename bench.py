@@ -172,10 +172,13 @@ def main():
     ap.add_argument("--eta", type=float, default=0.75)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--precision", choices=["fp32", "3xf16"], default="3xf16",
+    ap.add_argument("--precision", choices=["fp32", "3xf16", "f16"], default="3xf16",
                     help="conv arithmetic: the fp32-accurate 3xf16 split MFMA (default), or exact fp32 MFMA")
     ap.add_argument("--fp32-exact-steps", type=int, default=1,
                     help="N=1 only: also time this many steps in exact-fp32 mode (0 = skip)")
+    ap.add_argument("--f16-steps", type=int, default=1,
+                    help="N=1 only: also time this many steps in the reduced-precision f16 mode, reported separately "
+                         "(the reference's .half() experiment, code/test_quant.py:390-409; 0 = skip)")
     ap.add_argument("--workload", choices=["sample", "train"], default="sample",
                     help="sample: the headline DDIM-100 sampler (default); train: the training step (configs[4])")
     ap.add_argument("--noise", choices=["device", "parity"], default="device",
@@ -270,10 +273,12 @@ def main():
         d = conv_t[dom]  # launch durations measured live in the timed region
         conv = {k: v for k, v in (kernels or timed).items() if k.startswith("conv_")}
         achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
-        peak = PEAK_3XF16_TFLOPS if dom.startswith("conv_x3") else PEAK_FP32_TFLOPS
+        f16_1 = dom.startswith("conv_x3") and dom.endswith(",1>")  # the f16 mode: one product per MAC
+        peak = PEAK_F16_TFLOPS if f16_1 else (PEAK_3XF16_TFLOPS if dom.startswith("conv_x3") else PEAK_FP32_TFLOPS)
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4), "traffic": None, "kernel": dom,
-                    "peak_basis": ("dense f16 MFMA 2.5 PFLOP/s / 3 split products per fp32 MAC (algorithmic fp32 "
+                    "peak_basis": ("dense f16 MFMA 2.5 PFLOP/s (f16 mode: one product per MAC)" if f16_1 else
+                                   "dense f16 MFMA 2.5 PFLOP/s / 3 split products per fp32 MAC (algorithmic fp32 "
                                    "FLOP/s ceiling of the 3xf16 kernel)" if dom.startswith("conv_x3")
                                    else "dense fp32 MFMA (= fp32 vector rate)"),
                     "avg_launch_ms": d["ms"] / d["count"], "flops_per_launch": d["flops"] / d["count"],
@@ -328,6 +333,21 @@ def main():
         res["fp32_exact"] = {"value": round(B * args.fp32_exact_steps / el32, 4), "unit": "images/s",
                              "ms_per_step": round(el32 / args.fp32_exact_steps * 1e3, 2),
                              "steps": args.fp32_exact_steps, "warmup": 1, "dtype": "f32"}
+    if ws == 1 and args.precision == "3xf16" and args.f16_steps > 0:
+        # the reduced-precision variant (not fp32-class), same workload, timed separately
+        model.precision = "f16"
+        one_pass(0)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for i in range(args.f16_steps):
+            one_pass(1 + i)
+        torch.cuda.synchronize(dev)
+        el16 = time.perf_counter() - t1
+        model.precision = args.precision
+        res["f16_reduced"] = {"value": round(B * args.f16_steps / el16, 4), "unit": "images/s",
+                              "ms_per_step": round(el16 / args.f16_steps * 1e3, 2), "steps": args.f16_steps,
+                              "warmup": 1, "dtype": "f16 operands, fp32 accumulate (not fp32-class; "
+                                                    "tests/test_gpu_f16.py records its error)"}
     if rank == 0 and ws == 1 and args.cpu_baseline_seconds > 0:
         res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
     if rank == 0:

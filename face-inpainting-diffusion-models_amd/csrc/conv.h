@@ -87,6 +87,8 @@ struct ConvParams {
   // 3xf16 range guard (conv_x3.hip): set to 1 when an operand's magnitude reaches the f16 range
   // (|a| >= 65504 would split into inf). The host re-runs the eval in fp32 when it is set.
   unsigned* guard;
+  // split kernel products per MAC: 3 (IFD_PREC_3XF16, fp32-class) or 1 (IFD_PREC_F16, f16 operands)
+  int x3_nprod;
 };
 
 // Launch with the tile configuration chosen from (cout, taps, xform). Returns hipError_t.

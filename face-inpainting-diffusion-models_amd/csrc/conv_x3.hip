@@ -180,7 +180,7 @@ struct XSet {
   float vld[ITEMS];
 };
 
-template <int XF, bool SKIP, int TW>
+template <int XF, bool SKIP, int TW, int NPROD>
 struct XProducer {
   using Geo = XGeo<TW>;
   static constexpr int IT = Geo::ITEMS;
@@ -383,6 +383,16 @@ struct XProducer {
         gmax = fmaxf(gmax, fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
                                  fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
         unsigned h[4], l[4];
+        if (NPROD == 1) {  // f16 mode: the hi part only (one conversion per pair), no lo plane
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float a0 = v[2 * k], a1 = v[2 * k + 1];
+            asm volatile("" : "+v"(a0), "+v"(a1));
+            h[k] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0, a1}, f16x2));
+          }
+          *(lds_u4*)(As + 4 * ldso[i]) = u32x4{h[0], h[1], h[2], h[3]};
+          continue;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) split2(v[2 * k], v[2 * k + 1], h[k], l[k]);
         *(lds_u4*)(As + 4 * ldso[i]) = u32x4{h[0], h[1], h[2], h[3]};
@@ -398,7 +408,8 @@ __device__ __forceinline__ f32x16 xmfma(f16x8 a, f16x8 b, f32x16 c) {
 
 // MFMAs over one staged 3x3 chunk: 9 taps x (3 split products x 2 x 2 fragment blocks);
 // operand = the halo stage (planes of Geo::NP pixels, pb = halo pixel).
-template <int TW>
+// NPROD = 1 (the f16 precision mode): the hi x hi product only.
+template <int TW, int NPROD>
 __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws, const int (&pb)[2]) {
   using Geo = XGeo<TW>;
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
@@ -411,12 +422,12 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr) {
       ah[slot][mr] = *(const lds_h8*)(Ah + 4 * (pb[mr] + toff));
-      al[slot][mr] = *(const lds_h8*)(Al + 4 * (pb[mr] + toff));
+      if (NPROD == 3) al[slot][mr] = *(const lds_h8*)(Al + 4 * (pb[mr] + toff));
     }
 #pragma unroll
     for (int nr = 0; nr < 2; ++nr) {
       bs[slot][nr] = *(const lds_h8*)(Wb + 4 * (tap * 4 * XBN + nr * 32));
-      bl[slot][nr] = *(const lds_h8*)(Wb + 4 * (tap * 4 * XBN + 2 * XBN + nr * 32));
+      if (NPROD == 3) bl[slot][nr] = *(const lds_h8*)(Wb + 4 * (tap * 4 * XBN + 2 * XBN + nr * 32));
     }
   };
   fetch(0, 0);
@@ -431,6 +442,7 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
     __builtin_amdgcn_sched_barrier(0);
     if (tap + 1 < 9) fetch(tap + 1, cur ^ 1);
     __builtin_amdgcn_sched_barrier(0);
+    if (NPROD == 1) continue;
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
@@ -448,6 +460,7 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
 // One 1x1 skip chunk: the raw fp32 operand (pixel-major [256 px][4 swizzled quads][4] at As) is
 // split in registers with the producers' arithmetic (a_hi = f16(a), a_lo = f16(a - a_hi)), then
 // the 3 split products x 2 x 2 fragment blocks. pb = tile pixel.
+template <int NPROD>
 __device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws,
                                              const int (&pb)[2], float& gmax) {
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
@@ -476,6 +489,7 @@ __device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* A
   for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
     for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(ah[mr], bs[nr], acc[mr][nr]);
+  if (NPROD == 1) return;
 #pragma unroll
   for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
@@ -508,7 +522,7 @@ struct KCursor {
   }
 };
 
-template <int XF, bool SKIP, int TW>
+template <int XF, bool SKIP, int TW, int NPROD>
 __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   using Geo = XGeo<TW>;
   extern __shared__ __attribute__((aligned(16))) float smem_raw[];
@@ -685,9 +699,9 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       if (kk == nchu - 1 && S == 1 && X3_ABLATE < 9) prefetch(t);
       if (X3_ABLATE == 4) {
       } else if (!SKIP || cmain) {
-        consume_x3<TW>(acc, A0 + (j & 1) * XA, Ws, pb);
+        consume_x3<TW, NPROD>(acc, A0 + (j & 1) * XA, Ws, pb);
       } else {
-        consume_skip(acc, Ws + XSKA, Ws, pbs, gmax);
+        consume_skip<NPROD>(acc, Ws + XSKA, Ws, pbs, gmax);
       }
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
         p.trace[64 * blockIdx.x + 16 + j] = __builtin_amdgcn_s_memtime();
@@ -709,9 +723,9 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   // ---- producers: halo two chunks ahead in registers, weights (and skip operands) two chunks
   // ahead by LDS-DMA into a 3-slot ring (chunk j in slot j % 3) ----
   const int ptid = tid - NP_T;
-  XProducer<XF, SKIP, TW> P;
+  XProducer<XF, SKIP, TW, NPROD> P;
   P.init(ptid);
-  typename XProducer<XF, SKIP, TW>::Set s0, s1;
+  typename XProducer<XF, SKIP, TW, NPROD>::Set s0, s1;
   // Lookahead cursor over the chunk stream: position jl = (unit ul, chunk kl of the unit), the
   // unit's tile decoded once per unit; past the end it stays on the last chunk (re-issued loads /
   // DMA of identical bytes keep the op counts fixed).
@@ -722,7 +736,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   int lastmain = 1, prevmain = 1;  // the last / the previous issued chunk is a 3x3 chunk
   KCursor pc;
   int cmain = 1, cidx = 0;  // kind / index of the cursor's chunk (kept for the clamped repeats)
-  auto issue = [&](typename XProducer<XF, SKIP, TW>::Set& s) {  // DMA + register loads of the cursor's chunk, then advance
+  auto issue = [&](typename XProducer<XF, SKIP, TW, NPROD>::Set& s) {  // DMA + register loads of the cursor's chunk, then advance
     if (jl < J) {
       const int c = __builtin_amdgcn_readfirstlane(zl * nchu + kl);
       if (kl == 0) pc.reset();
@@ -796,27 +810,27 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   if (p.guard && P.gmax >= 65504.0f) atomicOr(p.guard, 1u);
 }
 
-template <int XF, bool SKIP, int TW>
+template <int XF, bool SKIP, int TW, int NPROD>
 static int launch_x3_inst(const ConvParams& p, hipStream_t stream) {
   static bool attr_set[kMaxDevices] = {};
   const size_t lds = (size_t)X_LDS_FLOATS * sizeof(float);
-  hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_x3_kernel<XF, SKIP, TW>), (int)lds);
+  hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_x3_kernel<XF, SKIP, TW, NPROD>), (int)lds);
   if (e != hipSuccess) return (int)e;
   const int ncu = device_cu_count();
   const int nunit = p.npix_tiles * (p.cout_pad / XBN) * p.ksplit;
   const int grid = nunit < ncu ? nunit : ncu;  // one workgroup per CU (LDS-bound)
-  hipLaunchKernelGGL((conv_x3_kernel<XF, SKIP, TW>), dim3(grid), dim3(NT), lds, stream, p);
+  hipLaunchKernelGGL((conv_x3_kernel<XF, SKIP, TW, NPROD>), dim3(grid), dim3(NT), lds, stream, p);
   return (int)hipGetLastError();
 }
 
-template <int TW>
+template <int TW, int NPROD>
 static int launch_x3_tw(const ConvParams& p, int xform, hipStream_t stream) {
   if (p.wskip) {
-    if (xform == XF_NONE) return launch_x3_inst<XF_NONE, true, TW>(p, stream);
+    if (xform == XF_NONE) return launch_x3_inst<XF_NONE, true, TW, NPROD>(p, stream);
     return (int)hipErrorInvalidValue;  // the skip segment comes with XF_NONE only (ResBlock conv2)
   }
-  if (xform == XF_NONE) return launch_x3_inst<XF_NONE, false, TW>(p, stream);
-  if (xform == XF_UP) return launch_x3_inst<XF_UP, false, TW>(p, stream);
+  if (xform == XF_NONE) return launch_x3_inst<XF_NONE, false, TW, NPROD>(p, stream);
+  if (xform == XF_UP) return launch_x3_inst<XF_UP, false, TW, NPROD>(p, stream);
   return (int)hipErrorInvalidValue;
 }
 
@@ -841,9 +855,15 @@ bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
 }
 
 int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream) {
-  if (p.TW == 32) return launch_x3_tw<32>(p, xform, stream);
-  if (p.TW == 16) return launch_x3_tw<16>(p, xform, stream);
-  if (p.TW == 8) return launch_x3_tw<8>(p, xform, stream);
+  if (p.x3_nprod == 1) {
+    if (p.TW == 32) return launch_x3_tw<32, 1>(p, xform, stream);
+    if (p.TW == 16) return launch_x3_tw<16, 1>(p, xform, stream);
+    if (p.TW == 8) return launch_x3_tw<8, 1>(p, xform, stream);
+    return (int)hipErrorInvalidValue;
+  }
+  if (p.TW == 32) return launch_x3_tw<32, 3>(p, xform, stream);
+  if (p.TW == 16) return launch_x3_tw<16, 3>(p, xform, stream);
+  if (p.TW == 8) return launch_x3_tw<8, 3>(p, xform, stream);
   return (int)hipErrorInvalidValue;
 }
 

@@ -390,7 +390,7 @@ int Model::guard_read(hipStream_t s, int* tripped) {
 }
 
 int Model::set_precision(int prec) {
-  IFD_REQUIRE(prec == IFD_PREC_FP32 || prec == IFD_PREC_3XF16, "unknown precision mode");
+  IFD_REQUIRE(prec == IFD_PREC_FP32 || prec == IFD_PREC_3XF16 || prec == IFD_PREC_F16, "unknown precision mode");
   prec_ = prec;
   return 0;
 }
@@ -646,6 +646,8 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   std::memset(&p, 0, sizeof(p));
   fill_opts(p);
   p.guard = guard_;
+  p.x3_nprod = prec_ == IFD_PREC_F16 ? 1 : 3;
+  const bool split_ = prec_ == IFD_PREC_3XF16 || prec_ == IFD_PREC_F16;  // the split-kernel modes
   p.in0 = in0; p.c0 = c0; p.in1 = in1; p.c1 = c1;
   p.N = N; p.Hin = Hin; p.Win = Hin; p.H = H; p.W = H;
   p.act = act; p.actA = A; p.actB = Bc;
@@ -662,7 +664,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   p.epi = epi;
   IFD_REQUIRE((H & (H - 1)) == 0, "spatial size must be a power of two");
   // the persistent split kernel: 256-pixel tiles, K split over units at low resolution
-  const bool x3_geo = prec_ == IFD_PREC_3XF16 && cw.x3_ok && epi == EPI_NHWC;
+  const bool x3_geo = split_ && cw.x3_ok && epi == EPI_NHWC;
   const int x3_chunks = (cw.cin_pad + (cw.has_skip ? cw.cs_pad : 0)) / 16;
   conv_geometry(p, H, H, N, cw.bn, x3_geo ? x3_chunks : cw.cin_pad / 8, x3_geo);
   if (epi != EPI_NHWC) p.ksplit = 1;
@@ -687,7 +689,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     return ((x3_off & 1) && g.TW == 16) || ((x3_off & 2) && g.ksplit > 1) || ((x3_off & 4) && cw.has_skip) ||
            ((x3_off & 8) && g.TW == 8) || ((x3_off & 16) && cw.taps == 1);
   };
-  if (prec_ == IFD_PREC_3XF16 && cw.taps == 1 && cw.x3_ok && cw.x3s_off && epi == EPI_NHWC && !in1 &&
+  if (split_ && cw.taps == 1 && cw.x3_ok && cw.x3s_off && epi == EPI_NHWC && !in1 &&
       xf == XF_NONE && !x3_masked_for(p)) {
     ConvParams q = p;
     q.in0 = nullptr; q.c0 = 0; q.in1 = nullptr; q.c1 = 0; q.cin_pad = 0; q.act = ACT_NONE;
@@ -709,7 +711,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   // 3xf16: the split kernel has no avg-pool prologue or residual; a down-ResBlock's convs read
   // act+pool(x) / pool(x) materialised by act_pool at the output resolution instead (the same
   // fp32 arithmetic as conv.hip's XF_DOWN paths)
-  if (prec_ == IFD_PREC_3XF16 && cw.x3_ok) {
+  if (split_ && cw.x3_ok) {
     const bool pool_in = xf == XF_DOWN && !in1;
     const bool pool_res = res && res_xf == XF_DOWN;
     ConvParams q = p;
@@ -747,7 +749,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     }
   }
   const bool x3_masked = x3_masked_for(p);
-  const bool use_x3 = prec_ == IFD_PREC_3XF16 && cw.x3_ok && !x3_masked && conv_x3_eligible(p, cw.taps, xf, cw.bn);
+  const bool use_x3 = split_ && cw.x3_ok && !x3_masked && conv_x3_eligible(p, cw.taps, xf, cw.bn);
   IFD_REQUIRE(use_x3 || p.cin_pad == cw.cin_pad, "1x1-only operand rewrite without the split kernel");
   if (use_x3) {
     p.wpack = wblob_ + cw.x3_off;
@@ -805,7 +807,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                use_x3 ? "conv_x3" : (use_head ? "conv_head" : (use_stream ? "conv_stream" : "conv_kernel")), p.bm,
                cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
     else if (use_x3)
-      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d>", xf, cw.has_skip ? "true" : "false", p.TW);
+      snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d,%d>", xf, cw.has_skip ? "true" : "false", p.TW, p.x3_nprod);
     else if (use_head)
       snprintf(nm, sizeof(nm), "conv_head_kernel<%d>", cw.cout);
     else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name

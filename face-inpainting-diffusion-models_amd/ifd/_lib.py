@@ -76,10 +76,20 @@ EXPORTS = {
     "ifd_to_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_void_p]),
     "ifd_mask_from_gray": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "ifd_resize_coeffs": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.POINTER(ctypes.c_int)]),
+    "ifd_resize_u8_workspace": (ctypes.c_int64, [ctypes.c_int64] + [ctypes.c_int] * 5),
+    "ifd_resize_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_int] * 5
+                      + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+    "ifd_image_to_float": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "ifd_make_inpaint_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 # conv arithmetic modes (include/ifd.h IFD_PREC_*)
-PRECISIONS = {"fp32": 0, "3xf16": 1}
+PRECISIONS = {"fp32": 0, "3xf16": 1, "f16": 2}
 
 _lib = None
 

@@ -77,6 +77,11 @@ int ifd_finalize(ifd_handle* h);
  * The reference has no such switch: its model runs in the caller's dtype (fp32 on this path). */
 #define IFD_PREC_FP32 0
 #define IFD_PREC_3XF16 1
+/* IFD_PREC_F16: the reduced-precision variant (the reference's `.half()` experiment,
+ * code/test_quant.py:390-409, reported separately): the split kernels with the hi parts only — f16
+ * operands, one f16 MFMA per MAC, fp32 accumulation; GroupNorm, attention, the head and the sampler
+ * update stay fp32. Not fp32-class: errors ~1e-3 relative per eval. */
+#define IFD_PREC_F16 2
 int ifd_set_precision(ifd_handle* h, int prec);
 /* 3xf16 range guard. The split needs every conv operand below the f16 range (|a| < 65504; the
  * weights are checked at finalize). The 3xf16 kernels set a device word when an operand reaches it
@@ -126,6 +131,23 @@ int ifd_to_u8(const float* sample, int64_t B, int C, int H, int W, uint8_t* out_
 /* Mask convention of OrderedMaskDataset (code/data/dataset.py:278-286): gray u8 (already resized)
  * -> mask fp32, 1 where gray/255 < 0.5 (black = hole), else 0. n elements, n == 0 is a no-op. */
 int ifd_mask_from_gray(const uint8_t* gray, int64_t n, float* mask, void* stream);
+
+/* Input-side data formats (OrderedMaskDataset / InpaintingDataset transforms, code/data/dataset.py:
+ * 231-240, 273-286) on the device. No GPU use by ifd_resize_coeffs / ifd_resize_u8_workspace.
+ *   ifd_resize_u8: Pillow BILINEAR resample (torchvision Resize((Hout, Wout)) of a PIL image), bit-exact,
+ *     NHWC uint8 [N,Hin,Win,C] -> [N,Hout,Wout,C]; `work` >= ifd_resize_u8_workspace(...) bytes.
+ *   ifd_resize_coeffs: the fixed-point coefficients (bounds[out][2] = first, count; coeffs[out][ksize]).
+ *   ifd_image_to_float: ToTensor + Normalize(0.5, 0.5): NHWC u8 -> NCHW fp32 in [-1, 1].
+ *   ifd_make_inpaint_batch: ordered mask cycling + mask rule + masked image for a batch: mask[n] =
+ *     (bank[idx[n] % M] / 255 < 0.5), masked_image = images * (1 - mask); bank u8 [M][H][W];
+ *     images / masked_image [N,3,H,W], mask [N,1,H,W] fp32 (either output may be NULL). */
+int ifd_resize_coeffs(int in_size, int out_size, int* bounds, int* coeffs, int* ksize);
+int64_t ifd_resize_u8_workspace(int64_t N, int C, int Hin, int Win, int Hout, int Wout);
+int ifd_resize_u8(const uint8_t* src, int64_t N, int C, int Hin, int Win, int Hout, int Wout, uint8_t* dst,
+                  uint8_t* work, int64_t work_bytes, void* stream);
+int ifd_image_to_float(const uint8_t* src_nhwc, int64_t N, int C, int H, int W, float* dst_nchw, void* stream);
+int ifd_make_inpaint_batch(const float* images, int64_t N, int H, int W, const uint8_t* mask_bank, int M,
+                           const int64_t* idx, float* mask, float* masked_image, void* stream);
 
 /* Per-launch profiler: when enabled, every kernel the handle launches is bracketed by hipEvents on
  * its stream; after the caller synchronises, ifd_profile_report writes a JSON summary per kernel

@@ -76,3 +76,21 @@ def test_train_host_helpers():
     n = L.ifd_tr_wgrad_part_floats(128, 128, 9, 2 * 64 * 64, c.byref(S))
     assert S.value >= 2 and n == S.value * 128 * 128 * 9
     assert L.ifd_tr_attention_bwd_scratch_floats(2, 16, 128) == 2 * 2 * 2 * 16 * 16
+
+
+@pytest.mark.parametrize("n_in,n_out", [(1024, 256), (300, 256), (64, 256), (256, 256), (31, 7)])
+def test_resize_coeffs_match_oracle(n_in, n_out):
+    """The library's Pillow-resample coefficients (host side, no GPU) equal the oracle's restatement,
+    which tests/test_cpu_data_oracle.py pins to Pillow itself."""
+    import numpy as np
+    from ifd import _lib
+    from oracle import ref_data
+    b_ref, k_ref, ks_ref = ref_data.precompute_coeffs(n_in, n_out)
+    L = _lib.lib()
+    ks = ctypes.c_int()
+    assert L.ifd_resize_coeffs(n_in, n_out, None, None, ctypes.byref(ks)) == 0 and ks.value == ks_ref
+    b = np.zeros(2 * n_out, np.int32)
+    k = np.zeros(n_out * ks.value, np.int32)
+    assert L.ifd_resize_coeffs(n_in, n_out, b.ctypes.data_as(ctypes.c_void_p), k.ctypes.data_as(ctypes.c_void_p),
+                               ctypes.byref(ks)) == 0
+    assert np.array_equal(b.reshape(-1, 2), b_ref) and np.array_equal(k.reshape(n_out, -1), k_ref)

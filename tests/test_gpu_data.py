@@ -57,3 +57,40 @@ def test_data_rejects_cpu_tensors():
         to_u8_device(torch.zeros(1, 3, 4, 4))
     with pytest.raises(RuntimeError):
         mask_from_gray(torch.zeros(1, 1, 4, 4, dtype=torch.uint8))
+
+
+# ---- input side (code/data/dataset.py:231-240, 273-286), against Pillow / the oracle ----------
+
+@pytest.mark.parametrize("hw,out,c", [((1024, 1024), (256, 256), 1), ((300, 200), (256, 256), 1),
+                                      ((64, 64), (256, 256), 1), ((97, 131), (64, 40), 3),
+                                      ((512, 384), (256, 256), 3), ((256, 256), (256, 256), 3),
+                                      ((31, 700), (256, 256), 3), ((256, 300), (256, 256), 1)])
+def test_resize_u8_matches_pillow(hw, out, c):
+    from PIL import Image
+    from ifd.data import resize_u8
+    rng = np.random.default_rng(sum(hw) * 7 + c)
+    imgs = rng.integers(0, 256, size=(2,) + hw + ((c,) if c == 3 else ()), dtype=np.uint8)
+    mode = "RGB" if c == 3 else "L"
+    ref = np.stack([np.asarray(Image.fromarray(a, mode).resize((out[1], out[0]), Image.BILINEAR)) for a in imgs])
+    got = resize_u8(torch.from_numpy(imgs).to(DEV), out[0], out[1]).cpu().numpy()
+    assert got.shape == ref.shape and np.array_equal(got, ref)
+
+
+def test_images_to_float_and_inpaint_batch():
+    from oracle import ref_data
+    from ifd.data import OrderedMaskBank, images_to_float
+    rng = np.random.default_rng(5)
+    u8 = rng.integers(0, 256, size=(5, 64, 64, 3), dtype=np.uint8)
+    x = images_to_float(torch.from_numpy(u8).to(DEV))
+    ref = np.stack([ref_data.to_tensor_normalize(a) for a in u8])
+    assert np.array_equal(x.cpu().numpy(), ref)
+    raw = [np.where(rng.random((h, w)) > 0.5, 255, 0).astype(np.uint8) for h, w in ((80, 80), (64, 64), (100, 37))]
+    bank = OrderedMaskBank(raw, img_size=64, device=DEV)
+    idx = [0, 1, 2, 3, 7]
+    b = bank.batch(x, idx)
+    for j, i in enumerate(idx):
+        g = ref_data.resize_u8(raw[ref_data.ordered_mask_index(i, 3)], 64, 64)
+        m = ref_data.mask_rule(g)
+        assert np.array_equal(b["mask"][j, 0].cpu().numpy(), m)
+        assert np.array_equal(b["masked_image"][j].cpu().numpy(), ref[j] * (1 - m)[None])
+    assert b["mask_idx"].tolist() == [0, 1, 2, 0, 1]
