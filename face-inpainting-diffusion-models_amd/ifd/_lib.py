@@ -40,6 +40,12 @@ class StepCoeffs(ctypes.Structure):
         "c_inj_a", "c_inj_b")] + [(n, ctypes.c_int) for n in ("use_noise", "inject", "clip", "pad")]
 
 
+class LibCoeffs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in (
+        "c_recip", "c_recipm1", "c_ab", "c_abp", "c_eta", "c_nonzero", "c_min_log", "c_max_log", "c_coef1",
+        "c_coef2")] + [(n, ctypes.c_int) for n in ("clip", "pad")]
+
+
 EXPORTS = {
     "ifd_create": (ctypes.c_int, [ctypes.POINTER(IfdConfig), ctypes.POINTER(ctypes.c_void_p)]),
     "ifd_destroy": (None, [ctypes.c_void_p]),
@@ -76,6 +82,11 @@ EXPORTS = {
     "ifd_to_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_void_p]),
     "ifd_mask_from_gray": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "ifd_lib_inject": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_float, ctypes.c_float, ctypes.c_int64]
+                       + [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p]),
+    "ifd_lib_update": (ctypes.c_int, [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                                                            ctypes.POINTER(LibCoeffs)]
+                       + [ctypes.c_void_p] * 3),
     "ifd_resize_coeffs": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.POINTER(ctypes.c_int)]),
     "ifd_resize_u8_workspace": (ctypes.c_int64, [ctypes.c_int64] + [ctypes.c_int] * 5),

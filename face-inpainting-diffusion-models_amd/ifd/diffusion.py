@@ -2,8 +2,13 @@
 
 Tables are float64 numpy (same formulas as code/gaussian_diffusion.py:47-80); per-timestep values
 are gathered in float64 and rounded to fp32 once (`_extract_into_tensor`,
-code/gaussian_diffusion.py:12-24). The per-pixel work of the library loops is small elementwise
-algebra around the model call; it runs as torch ops on whatever device the model runs on.
+code/gaussian_diffusion.py:12-24).
+The library loops (p_sample_loop / ddim_sample_loop and their _progressive forms) run each step's
+algebra as two HIP kernels on GPU tensors (include/ifd.h ifd_lib_inject / ifd_lib_update): the
+known-region injection before the model call and the DDIM / DDPM update after it, with the
+step's coefficients taken on the host from the loop's own timestep, so there is no
+`int(t[0].item())` sync per step. Direct calls of the per-step API (ddim_sample, p_sample,
+apply_inpainting_injection, p_mean_variance, ...) with arbitrary t keep the reference's torch algebra.
 The headline path (the scripts' DDIM / DDPM loops) does NOT go through here: it is fused into the
 UNet's last conv by `ifd.sampler` (ifd_ddim_step / ifd_ddpm_step).
 """
@@ -12,7 +17,12 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import _lib
 from .losses import LossType, ModelMeanType, ModelVarType
+
+
+def _f32(v):
+    return float(np.float32(v))
 
 
 def _extract_into_tensor(arr, timesteps, broadcast_shape):
@@ -63,25 +73,47 @@ class GaussianDiffusion:
         return torch.randn(*shape, device=self.noise_device).to(device)
 
     # ---- known-region injection (code/gaussian_diffusion.py:85-157) --------------------------
-    def get_gt_noised(self, gt, timestep):
+    def _gt_noise(self, gt, timestep):
         key = (gt.shape, timestep, gt.device)
         noise = self._gt_noises_cache.get(key)
         if noise is None:
             noise = self._randn_like(gt)
             self._gt_noises_cache[key] = noise
+        return noise
+
+    def get_gt_noised(self, gt, timestep):
+        noise = self._gt_noise(gt, timestep)
         t = torch.tensor([timestep], device=gt.device).expand(gt.shape[0])
         return self.q_sample(gt, t, noise=noise)
 
     def clear_gt_noise_cache(self):
         self._gt_noises_cache.clear()
 
-    def apply_inpainting_injection(self, x, t, gt, gt_keep_mask, use_cumulative_noise=True, injection_schedule="all"):
+    def apply_inpainting_injection(self, x, t, gt, gt_keep_mask, use_cumulative_noise=True, injection_schedule="all",
+                                   _tau=None):
         if gt is None or gt_keep_mask is None:
             return x
-        tau = int(t[0].item())
+        tau = int(t[0].item()) if _tau is None else int(_tau)  # the library loops pass their host timestep
         half = self.num_timesteps // 2
         if (injection_schedule == "high" and tau < half) or (injection_schedule == "low" and tau >= half):
             return x
+        B, C, H, W = x.shape
+        if (_tau is not None and x.is_cuda and x.dtype == torch.float32 and gt.shape == x.shape
+                and tuple(gt_keep_mask.shape) in ((B, 1, H, W), (1, 1, H, W))):
+            # fused: keep * q_sample(gt) + (1 - keep) * x in one kernel (coefficients as _extract yields them)
+            if use_cumulative_noise:
+                noise = self._gt_noise(gt, tau)
+                ca, cb = _f32(self.sqrt_alphas_cumprod[tau]), _f32(self.sqrt_one_minus_alphas_cumprod[tau])
+            else:
+                ac = np.float32(self.alphas_cumprod[tau])
+                ca, cb = float(np.sqrt(ac)), float(np.sqrt(np.float32(1) - ac))
+                noise = self._randn_like(gt)
+            keep = gt_keep_mask.to(torch.float32).expand(B, 1, H, W).contiguous()
+            out = torch.empty_like(x)
+            xc, gc, nc = x.contiguous(), gt.to(torch.float32).contiguous(), noise.contiguous()
+            _lib.check(_lib.lib().ifd_lib_inject(_lib.ptr(xc), _lib.ptr(gc), _lib.ptr(keep), _lib.ptr(nc), ca, cb, B, C, H,
+                                                 W, _lib.ptr(out), _lib.stream_ptr(x.device)))
+            return out
         if use_cumulative_noise:
             weighed = self.get_gt_noised(gt, tau)
         else:
@@ -190,17 +222,46 @@ class GaussianDiffusion:
         out["mean"], _, _ = self.q_posterior_mean_variance(x_start=out["pred_xstart"], x_t=x, t=t)
         return out
 
-    def _maybe_inject(self, x, t, model_kwargs, use_inpainting_injection, injection_schedule, use_cumulative_noise):
+    def _maybe_inject(self, x, t, model_kwargs, use_inpainting_injection, injection_schedule, use_cumulative_noise,
+                      _tau=None):
         if use_inpainting_injection and model_kwargs:
             gt, keep = model_kwargs.get("gt"), model_kwargs.get("gt_keep_mask")
             if gt is not None and keep is not None:
                 return self.apply_inpainting_injection(x, t, gt, keep, use_cumulative_noise=use_cumulative_noise,
-                                                       injection_schedule=injection_schedule)
+                                                       injection_schedule=injection_schedule, _tau=_tau)
         return x
 
+    def _fused_step(self, ddim, model, x, t, tau, clip_denoised, model_kwargs, eta=0.0):
+        """One library-loop step's update as one HIP kernel (x and the model output on the GPU, EPSILON
+        mean, LEARNED_RANGE variance). Draws the step noise in the reference's order (after the model)."""
+        B, C, H, W = x.shape
+        out = model(x, self._scale_timesteps(t), **(model_kwargs or {}))
+        assert out.shape == (B, C * 2, H, W)
+        noise = self._randn_like(x)
+        c = _lib.LibCoeffs()
+        c.c_recip, c.c_recipm1 = _f32(self.sqrt_recip_alphas_cumprod[tau]), _f32(self.sqrt_recipm1_alphas_cumprod[tau])
+        c.c_ab, c.c_abp, c.c_eta = _f32(self.alphas_cumprod[tau]), _f32(self.alphas_cumprod_prev[tau]), _f32(eta)
+        c.c_nonzero = 1.0 if tau != 0 else 0.0
+        c.c_min_log, c.c_max_log = _f32(self.posterior_log_variance_clipped[tau]), _f32(np.log(self.betas)[tau])
+        c.c_coef1, c.c_coef2 = _f32(self.posterior_mean_coef1[tau]), _f32(self.posterior_mean_coef2[tau])
+        c.clip = int(bool(clip_denoised))
+        xc, oc, nc = x.contiguous(), out.to(torch.float32).contiguous(), noise.contiguous()
+        sample, pred = torch.empty_like(xc), torch.empty_like(xc)
+        _lib.check(_lib.lib().ifd_lib_update(int(ddim), _lib.ptr(xc), _lib.ptr(oc), _lib.ptr(nc), B, H, W, c,
+                                             _lib.ptr(sample), _lib.ptr(pred), _lib.stream_ptr(x.device)))
+        return {"sample": sample, "pred_xstart": pred}
+
+    def _can_fuse(self, x, cond_fn, denoised_fn, _tau):
+        return (_tau is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == 3
+                and cond_fn is None and denoised_fn is None and self.model_mean_type == ModelMeanType.EPSILON
+                and self.model_var_type == ModelVarType.LEARNED_RANGE)
+
     def p_sample(self, model, x, t, clip_denoised=True, denoised_fn=None, cond_fn=None, model_kwargs=None,
-                 use_inpainting_injection=False, injection_schedule="all", use_cumulative_noise=True):
-        x = self._maybe_inject(x, t, model_kwargs, use_inpainting_injection, injection_schedule, use_cumulative_noise)
+                 use_inpainting_injection=False, injection_schedule="all", use_cumulative_noise=True, _tau=None):
+        x = self._maybe_inject(x, t, model_kwargs, use_inpainting_injection, injection_schedule, use_cumulative_noise,
+                               _tau)
+        if self._can_fuse(x, cond_fn, denoised_fn, _tau):
+            return self._fused_step(False, model, x, t, int(_tau), clip_denoised, model_kwargs)
         out = self.p_mean_variance(model, x, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
                                    model_kwargs=model_kwargs)
         noise = self._randn_like(x)
@@ -222,7 +283,7 @@ class GaussianDiffusion:
         for i in indices:
             t = torch.tensor([i] * shape[0], device=device)
             with torch.no_grad():
-                out = step(model, img, t, **kw)
+                out = step(model, img, t, _tau=i, **kw)
                 yield out
                 img = out["sample"]
 
@@ -249,8 +310,11 @@ class GaussianDiffusion:
                                      injection_schedule=injection_schedule, use_cumulative_noise=use_cumulative_noise)
 
     def ddim_sample(self, model, x, t, clip_denoised=True, denoised_fn=None, cond_fn=None, model_kwargs=None, eta=0.0,
-                    use_inpainting_injection=False, injection_schedule="all", use_cumulative_noise=True):
-        x = self._maybe_inject(x, t, model_kwargs, use_inpainting_injection, injection_schedule, use_cumulative_noise)
+                    use_inpainting_injection=False, injection_schedule="all", use_cumulative_noise=True, _tau=None):
+        x = self._maybe_inject(x, t, model_kwargs, use_inpainting_injection, injection_schedule, use_cumulative_noise,
+                               _tau)
+        if self._can_fuse(x, cond_fn, denoised_fn, _tau):
+            return self._fused_step(True, model, x, t, int(_tau), clip_denoised, model_kwargs, eta)
         out = self.p_mean_variance(model, x, t, clip_denoised=clip_denoised, denoised_fn=denoised_fn,
                                    model_kwargs=model_kwargs)
         if cond_fn is not None:

@@ -132,6 +132,24 @@ int ifd_to_u8(const float* sample, int64_t B, int C, int H, int W, uint8_t* out_
  * -> mask fp32, 1 where gray/255 < 0.5 (black = hole), else 0. n elements, n == 0 is a no-op. */
 int ifd_mask_from_gray(const uint8_t* gray, int64_t n, float* mask, void* stream);
 
+/* Library loops (GaussianDiffusion.p_sample_loop / ddim_sample_loop, code/gaussian_diffusion.py:357-538):
+ *   ifd_lib_inject: apply_inpainting_injection (:114-157): out = keep * (ca * gt + cb * noise) + (1 - keep) * x,
+ *     keep [B,1,H,W] broadcast over C; ca, cb the fp32 q_sample coefficients of the step (cached-noise
+ *     path: sqrt_alphas_cumprod / sqrt_one_minus; fresh-noise path: fp32 sqrt of the extracted ac).
+ *   ifd_lib_update: ddim != 0: ddim_sample (:447-485), else p_sample (:357-388), from the model output
+ *     out6 [B,6,H,W] (eps, learned-range v) and the step noise: sample (and pred_xstart, may be NULL). */
+typedef struct ifd_lib_coeffs {
+  float c_recip, c_recipm1;   /* sqrt_recip_alphas_cumprod[t], sqrt_recipm1_alphas_cumprod[t] */
+  float c_ab, c_abp, c_eta;   /* DDIM: alphas_cumprod[t], alphas_cumprod_prev[t], eta */
+  float c_nonzero;            /* (t != 0) */
+  float c_min_log, c_max_log, c_coef1, c_coef2;  /* DDPM: posterior_log_variance_clipped, log(betas), coefs */
+  int clip, pad;
+} ifd_lib_coeffs;
+int ifd_lib_inject(const float* x, const float* gt, const float* keep, const float* noise, float ca, float cb,
+                   int64_t B, int C, int H, int W, float* out, void* stream);
+int ifd_lib_update(int ddim, const float* x, const float* out6, const float* noise, int64_t B, int H, int W,
+                   const ifd_lib_coeffs* c, float* sample, float* pred_xstart, void* stream);
+
 /* Input-side data formats (OrderedMaskDataset / InpaintingDataset transforms, code/data/dataset.py:
  * 231-240, 273-286) on the device. No GPU use by ifd_resize_coeffs / ifd_resize_u8_workspace.
  *   ifd_resize_u8: Pillow BILINEAR resample (torchvision Resize((Hout, Wout)) of a PIL image), bit-exact,

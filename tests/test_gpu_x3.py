@@ -111,7 +111,7 @@ def test_x3_matches_fp32_batch4(x3_model):
         y3, ks = _kernels_run(x3_model, lambda: x3_model(x, t, masked_image=gt * (1 - mask), mask=mask))
         y32 = m32(x, t, masked_image=gt * (1 - mask), mask=mask)
         y1 = x3_model(x[2:3], t[2:3], masked_image=(gt * (1 - mask))[2:3], mask=mask[2:3])
-    assert any(k.startswith("conv_x3_kernel") and k.endswith(",8>") for k in ks), sorted(ks)
+    assert any(k.startswith("conv_x3_kernel") and k.endswith(",8,3>") for k in ks), sorted(ks)
     assert torch.isfinite(y3).all()
     err = maxabs(y3, y32)
     print(f"3xf16 vs fp32 B=4 maxabs={err:.3g}")
