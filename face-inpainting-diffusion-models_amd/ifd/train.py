@@ -506,3 +506,60 @@ class UNetTrainer:
         self.backward(self._dout6)
         self.optimizer_step()
         return loss
+
+
+class BlockTrainer(UNetTrainer):
+    """Forward + backward of ONE block of the UNet on the same training ops (a per-block entry point:
+    ResBlock, code/nn.py:136-212 — plain, with 1x1 skip, down, up — or AttentionBlock, :238-265).
+    Parameter names are the reference module's own state_dict keys (no prefix). Tensors NCHW at the
+    boundary, NHWC inside."""
+
+    def __init__(self, kind, cin, cout, emb_dim=None, device="cuda", num_head_channels=64):
+        from types import SimpleNamespace
+        from .topology import _attn_params, _res_params
+        self.dev = torch.device(device)
+        self.kind, self.cin, self.cout = kind, cin, cout
+        self.emb_dim = emb_dim
+        self.cfg = SimpleNamespace(num_head_channels=num_head_channels, model_channels=0, out_channels=cout)
+        spec = _res_params("", cin, cout, emb_dim) if kind.startswith("res") else _attn_params("", cin)
+        self.spec = [(k, tuple(s)) for k, s in spec]
+        self.offsets, n = {}, 0
+        for k, shape in self.spec:
+            self.offsets[k] = (n, shape)
+            n += int(np.prod(shape))
+        self.numel = n
+        self.flat = torch.zeros(n, device=self.dev)
+        self.grad = torch.zeros(n, device=self.dev)
+        self._zero_bias = torch.zeros(4096, device=self.dev)
+        self._pack_cache = {}
+        self.s = None
+
+    def load_state_dict(self, sd):
+        with torch.no_grad():
+            for k, _ in self.spec:
+                self.p(k).copy_(torch.as_tensor(sd[k]).to(self.dev, torch.float32).reshape(self.p(k).shape))
+
+    def forward_block(self, x, emb=None):
+        self.s = _lib.stream_ptr(self.dev)
+        self._pack_cache = {}
+        N, C, H, _ = x.shape
+        xh = x.to(self.dev, torch.float32).permute(0, 2, 3, 1).contiguous()
+        self._saved = {}
+        L = dict(kind=self.kind, prefix="", cin=self.cin, cout=self.cout)
+        if self.kind.startswith("res"):
+            e = emb.to(self.dev, torch.float32).contiguous()
+            self._tape = {"emb": e}
+            y, r = self._res_fwd(L, xh, N, H, e, self._saved)
+        else:
+            y, r = self._attn_fwd(L, xh, N, H, self._saved), H
+        self._N, self._r, self._rin = N, r, H
+        return y.view(N, r, r, -1).permute(0, 3, 1, 2).contiguous()
+
+    def backward_block(self, dy):
+        N = self._N
+        dyh = dy.to(self.dev, torch.float32).permute(0, 2, 3, 1).contiguous()
+        L = dict(kind=self.kind, prefix="", cin=self.cin, cout=self.cout)
+        demb = self._zeros(N, self.emb_dim) if self.kind.startswith("res") else None
+        dx, _ = self._layer_bwd(L, dyh, N, self._saved, demb)
+        dx = dx.view(N, self._rin, self._rin, self.cin)
+        return dx.permute(0, 3, 1, 2).contiguous(), demb

@@ -35,11 +35,6 @@ def loops():
 
 
 @pytest.fixture(scope="session")
-def layers():
-    return dict(np.load(os.path.join(GOLDEN, "layers.npz")))
-
-
-@pytest.fixture(scope="session")
 def meta_full():
     with open(os.path.join(GOLDEN, "full", "meta_full.json")) as f:
         return json.load(f)

@@ -172,8 +172,9 @@ def main():
             yo = ref_unet.attention(sd, "", x, 64)
         meta["checks"][f"oracle_vs_ref_{name}"] = maxabs(y, yo)
         layers[name] = dict(x=x, y=y, **{"w." + k: v for k, v in sd.items()})
-    np.savez_compressed(os.path.join(OUT, "layers.npz"),
-                        **{f"{n}/{k}": v.numpy() for n, d in layers.items() for k, v in d.items()})
+    # (round 1 stored these forward-only tensors as layers.npz; the block-level fixtures, forward and
+    # backward, are now made by make_golden_blocks.py — only the oracle checks are kept here)
+    del layers
 
     # ---------- 3. whole-UNet evals ----------
     evals = {}
