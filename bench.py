@@ -50,31 +50,41 @@ def synth_inputs(B, H, seed, device):
     return gt.to(device), mask.to(device)
 
 
+class _BudgetSpent(Exception):
+    pass
+
+
 def cpu_baseline(budget_s, H=256):
-    """The oracle (pure-torch CPU restatement of the reference UNet, pinned bit-exact to it by
-    tests/golden) timed on this host's cores: B=1 256x256 UNet evals until `budget_s` elapses,
-    extrapolated x101 evals per DDIM-100 image (the update algebra is < 0.1 % of an eval)."""
+    """The oracle (pure-torch CPU restatement of the reference, pinned bit-exact to it by tests/golden)
+    timed on this host's cores: the reference's own DDIM-100 script loop (oracle script_ddim_loop =
+    code/test_inp_ddim_100.py:470-576: model_fn, UNet, DDIM update, injection) at B=1 256x256, run
+    step by step until `budget_s` elapses. Per-step time = the span between the first and the last
+    completed step's model call (the first step is warm-up); images/s = 1 / (101 x per-step)."""
     from ifd.manifest import make_state_dict
     from ifd.topology import FULL
-    from oracle import ref_unet
+    from oracle import ref_diffusion, ref_unet
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(cores)
     sd = ref_unet.strip_prefix(make_state_dict(FULL, seed=1))
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(1, 3, H, H, generator=g)
-    gt = torch.rand(1, 3, H, H, generator=g) * 2 - 1
-    mask = torch.zeros(1, 1, H, H)
-    mask[:, :, H // 4: 3 * H // 4, H // 4: 3 * H // 4] = 1
-    t = torch.tensor([500])
-    times = []
-    t_start = time.time()
+    tb = ref_diffusion.Tables(ref_diffusion.get_named_beta_schedule("cosine", 1000))
+    torch.manual_seed(0)
+    gt, mask = synth_inputs(1, H, seed=7, device="cpu")
+    stamps = []
+
+    def unet_call(x, t, masked, m):
+        stamps.append(time.time())
+        if len(stamps) >= 3 and (stamps[-1] - stamps[0] > budget_s or len(stamps) > 101):
+            raise _BudgetSpent
+        return ref_unet.inpaint_forward(sd, x, t, masked, m, FULL)
     with torch.no_grad():
-        while len(times) < 2 or (time.time() - t_start < budget_s and len(times) < 64):
-            t0 = time.time()
-            ref_unet.inpaint_forward(sd, x, t, gt * (1 - mask), mask, FULL)
-            times.append(time.time() - t0)
-    times = sorted(times[1:]) if len(times) > 2 else times
-    t_eval = times[len(times) // 2]
+        try:
+            ref_diffusion.script_ddim_loop(tb, ref_diffusion.model_fn_factory(unet_call), (1, 3, H, H), gt, mask,
+                                           100, clip=True, eta=0.75)
+            stamps.append(time.time())
+        except _BudgetSpent:
+            pass
+    steps = len(stamps) - 2  # complete steps between the 2nd model call and the last stamp
+    t_step = (stamps[-1] - stamps[1]) / steps
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -83,10 +93,28 @@ def cpu_baseline(budget_s, H=256):
                 break
     except OSError:
         pass
-    return {"value": 1.0 / (101 * t_eval), "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": f"{len(times)} B=1 256x256 UNet evals of oracle/ref_unet.py (torch CPU fp32), median "
-                      f"{t_eval * 1e3:.0f} ms/eval, x101 evals per DDIM-100 image",
-            "s_per_unet_eval": t_eval, "cpu_model": cpu_model}
+    return {"value": 1.0 / (101 * t_step), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": f"{steps} timed steps (after 1 warm-up) of the oracle's DDIM-100 cosine script loop "
+                      f"(oracle/ref_diffusion.script_ddim_loop + ref_unet, torch CPU fp32) at B=1 256x256, "
+                      f"{t_step * 1e3:.0f} ms/step, x101 steps per image",
+            "s_per_step": t_step, "cpu_model": cpu_model}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch and MFMA-busy fraction of `kernel` from the newest committed PMC summary
+    (profiles/<tag>/pmc_summary.json, written by tools/gpu_round.sh: separate rocprofv3 --pmc passes over
+    this same bench command, FETCH_SIZE x2 / WRITE_SIZE x1 per tools/micro/pmc_cal.hip). PMC counters
+    cannot be read inside a live run without the profiler, so the live line cites that file."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), reverse=True):
+        try:
+            k = json.load(open(path))["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k and k.get("hbm_bytes_per_launch"):
+            return {"traffic": k["hbm_bytes_per_launch"], "mfma_busy": k.get("mfma_busy_frac"),
+                    "traffic_source": os.path.relpath(path, ROOT)}
+    return {"traffic": None}
 
 
 def _free_port():
@@ -283,6 +311,9 @@ def main():
                                    else "dense fp32 MFMA (= fp32 vector rate)"),
                     "avg_launch_ms": d["ms"] / d["count"], "flops_per_launch": d["flops"] / d["count"],
                     "algorithmic_bytes_per_launch": d["bytes"] / d["count"], "launches": int(d["count"])}
+        roofline.update(pmc_traffic(dom))
+        if roofline["traffic"]:
+            roofline["traffic_over_algorithmic"] = round(roofline["traffic"] / roofline["algorithmic_bytes_per_launch"], 3)
         tot_ms = sum(v["ms"] for v in (kernels or timed).values())
         conv_flops = sum(v["flops"] for v in conv.values())
         conv_ms = sum(v["ms"] for v in conv.values())

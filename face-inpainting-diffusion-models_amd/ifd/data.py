@@ -1,7 +1,8 @@
 """Data formats either side of the sampler, on the HIP library.
 
-* `toU8` mirrors code/test_inp_ddim_50.py:33-41: [B,C,H,W] fp32 in [-1,1] -> numpy uint8 [B,H,W,C]
-  (None passes through). `to_u8_device` keeps the result on the GPU.
+* `toU8` mirrors code/test_inp_ddim_50.py:33-41: [B,C,H,W] float in [-1,1] -> numpy uint8 [B,H,W,C]
+  (None passes through; CPU or non-fp32 inputs are moved to the GPU as fp32 first — the
+  conversion itself always runs on the HIP kernel). `to_u8_device` keeps the result on the GPU.
 * `mask_from_gray` is the mask convention of OrderedMaskDataset (code/data/dataset.py:278-286):
   a grayscale uint8 mask, already resized, -> fp32 mask, 1 = hole (black), 0 = keep (white).
   `masked_image` is image * (1 - mask) (dataset.py:289), the same arithmetic as model_fn.
@@ -32,10 +33,16 @@ def to_u8_device(sample: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def toU8(sample):
+def toU8(sample, device=None):
+    """Like the reference's toU8, any float dtype and any device: the tensor is moved to the GPU
+    (`device`, default the current one) as fp32 and converted there by the HIP kernel."""
     if sample is None:
         return sample
-    return to_u8_device(sample.detach()).cpu().numpy()
+    x = sample.detach()
+    if not x.is_cuda or x.dtype != torch.float32:
+        x = x.to(device=device if device is not None else ("cuda" if not x.is_cuda else x.device),
+                 dtype=torch.float32)
+    return to_u8_device(x).cpu().numpy()
 
 
 def mask_from_gray(gray: torch.Tensor) -> torch.Tensor:

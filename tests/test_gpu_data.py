@@ -30,6 +30,16 @@ def test_to_u8_bitexact(shape):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float64, torch.float32])
+def test_to_u8_cpu_and_other_dtypes(dtype):
+    """The reference's toU8 takes any device / float dtype; ours moves the tensor to the GPU as fp32
+    (the conversion runs in fp32, so the expectation is the reference expression on x.float())."""
+    from ifd.data import toU8
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(2, 3, 9, 11, generator=g) * 2.2 - 1.1).to(dtype)
+    assert np.array_equal(toU8(x, device=DEV), ref_to_u8(x.float()))
+
+
 def test_to_u8_empty_and_none():
     from ifd.data import toU8
     assert toU8(None) is None
