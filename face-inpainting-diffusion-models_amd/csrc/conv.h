@@ -84,6 +84,7 @@ struct ConvParams {
   // batch-invariant geometry (split-K and tile kind chosen per image, not per batch, so an image's
   // result does not depend on how many other images share the launch)
   int opt_bm128, opt_lds_pad, opt_stream_cw, opt_invariant;
+  int opt_x3_order;  // split kernel unit order: 0 auto, 1 XCD-concurrent channel tiles, 2 = 1 for skip layers only
   // 3xf16 range guard (conv_x3.hip): set to 1 when an operand's magnitude reaches the f16 range
   // (|a| >= 65504 would split into inf). The host re-runs the eval in fp32 when it is set.
   unsigned* guard;

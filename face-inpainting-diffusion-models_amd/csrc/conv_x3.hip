@@ -29,10 +29,12 @@
 //   * waves 4-7 producers: halo of chunk j+2 in registers (buffer descriptors, no per-chunk VALU
 //     address work), weights of chunk j+2 by LDS-DMA, prologue of chunk j+1 (GroupNorm-apply
 //     [+ scale/shift] + SiLU, nearest-up, zero padding) + the f16 split, LDS writes.
-//   * a ResBlock's 1x1 skip segment (the chunks after the 3x3 ones): the producers LDS-DMA the raw
-//     block input into the spare 32 KiB of the chunk's weight-ring slot and the consumers split it
-//     in registers: a 1x1 chunk is too short (12 MFMAs) to hide register-staged loads two chunks
-//     ahead, and the DMA needs no producer registers or VALU.
+//   * a ResBlock's 1x1 skip segment (the chunks after the 3x3 ones, XSK channels each): the
+//     producers LDS-DMA only the chunk's weight slab into the ring; the raw fp32 operand goes
+//     straight from HBM into the consumer waves' registers (no wave shares a pixel row of the 1x1
+//     operand, so LDS staging buys no reuse), two chunks deep: the two lanes of a pixel load its
+//     XSK x 4 B as whole cache lines, the first chunks during the unit's last 3x3 chunk, then chunk
+//     s + 2 while chunk s is split and consumed.
 // LDS: A = 4 planes [part hi/lo][channel half h][halo px][8 f16] (<= 21.25 KiB) double-buffered,
 // W = [tap][part][h][64 co][8 f16] (36 KiB) in a 3-slot ring (DMA two chunks ahead).
 #include "conv.h"
@@ -41,9 +43,8 @@
 // Timing-only ablation builds (never shipped; outputs are garbage): X3_ABLATE=
 //   1 producers skip the halo loads and LDS writes (weights DMA + barriers only)
 //   2 producers load the halo but skip the prologue / split / LDS writes
-//   4 consumers idle (barriers only)      5 no weight DMA
-//   8 producers idle (no DMA, no halo)   9 = 8 + no consumer epilogue   10 = 9 + no barriers
-//   11 skip chunks DMA the weights in place of the operand gather
+//   4 consumers skip the 3x3 MFMAs        5 no weight DMA
+//   8 producers idle (no DMA, no halo)   12 skip operands all read from one tile (cache-resident)
 #ifndef X3_ABLATE
 #define X3_ABLATE 0
 #endif
@@ -87,10 +88,13 @@ constexpr int XA = 4 * XNPMAX * 4;             // floats per A stage (4 planes x
 constexpr int XW = 9 * 2 * 2 * XBN * 4;        // floats per weight-ring slot (36 KiB)
 constexpr int XWDMA = XW / 4 / NP_T;           // 16-B LDS-DMA rounds per producer thread (9)
 constexpr int X_LDS_FLOATS = 2 * XA + 3 * XW;  // 40448 floats = 158 KiB
-constexpr int XSKA = 1024;                     // skip chunk slot: weights [0, XSKA), operand planes after
+constexpr int XSK = 32;                        // channels per 1x1 skip chunk
+constexpr int XSQ = XSK / 16;                  // k = 16 MFMA steps (sub-chunks) per skip chunk
+constexpr int XSL = XSQ * 2;                   // operand quads per lane (channel half: XSK / 2 channels)
+constexpr int XWS = XSQ * 2 * 2 * XBN * 4;     // floats per skip weight slab [q][part][h][64 co][8 f16]
 constexpr float kLo = 2048.0f;                 // 2^11
-static_assert(XW % (4 * NP_T) == 0, "weight slab must be whole DMA rounds");
-static_assert(XSKA + 2 * 4096 <= XW, "skip chunk slot layout");
+static_assert(XW % (4 * NP_T) == 0 && XWS % (4 * NP_T) == 0, "weight slabs must be whole DMA rounds");
+static_assert(XWS <= XW, "skip slab fits a ring slot");
 
 #define XBARRIER_CONSUMER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #define XBARRIER_PRODUCER(N) asm volatile("s_waitcnt vmcnt(" #N ") lgkmcnt(0)\n\ts_barrier" ::: "memory")
@@ -108,11 +112,10 @@ struct XGeo {
   static constexpr int LOADS = 2 * ITEMS + 4;               // register loads per 3x3 chunk (vmcnt arithmetic)
   static_assert(NP <= XNPMAX && (ITEMS == 3 || (IMG == 4 && ITEMS == 4)), "halo staging items");
 };
-// vmcnt ops per chunk, in issue order: a 3x3 chunk = XDMA3 weight DMAs then XGeo::LOADS halo /
-// coefficient register loads; a skip chunk = XDMA1 DMAs (weights, operand) and no register load
-// (the barrier's vmcnt arithmetic). (An L2 prefetch of later skip operands - one line request per
-// tile pixel - measured slower at distances 4 to 8: it holds miss slots the gathers need.)
-constexpr int XDMA3 = 9, XDMA1 = 5;
+// vmcnt ops per chunk of a producer thread, in issue order: a 3x3 chunk = XDMA3 weight DMAs then
+// XGeo::LOADS halo / coefficient register loads; a skip chunk = XDMA1 weight DMAs and no register
+// load (the barrier's vmcnt arithmetic).
+constexpr int XDMA3 = 9, XDMA1 = XWS / 4 / NP_T;
 
 // Work unit L -> (tile, split z). The S splits of a tile are consecutive L; pixel tiles in groups
 // of 8 get channel-tile IDs 8 apart (conv.hip's XCD-aware map) when the tile count allows. Every
@@ -127,9 +130,10 @@ struct XDec {
 };
 __device__ __forceinline__ XDec x3_dec(const ConvParams& p, int nct) {
   const bool pow2 = (nct & (nct - 1)) == 0;
+  const bool order_ok = p.opt_x3_order == 0 || (p.opt_x3_order == 2 && !p.wskip);
   return {__builtin_ctz(p.ksplit), __builtin_ctz(nct), __builtin_ctz(p.tiles_x), __builtin_ctz(p.tiles_y),
-          __builtin_ctz(p.IMGS), pow2 && p.npix_tiles % 8 == 0, p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0,
-          nct, pow2};
+          __builtin_ctz(p.IMGS), pow2 && p.npix_tiles % 8 == 0,
+          order_ok && p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0, nct, pow2};
 }
 // Unit u of block b. blk_major (no split-K, pixel tiles a multiple of the grid): block b takes
 // pixel tiles b, b + G, ... and runs all channel tiles of each back to back, so the second
@@ -194,14 +198,9 @@ struct XProducer {
   int cur_unit = -1;
   rsrc_t r0, r1, ra, rb;
   int off0[IT], off1[IT];
-  int tn0;
-  // Skip segment (per unit). Skip chunks issue DMA only - no register load, no per-chunk VALU: a
-  // dead placeholder load frees its VGPRs for VALU temporaries, the compiler then waits (vmcnt) for
-  // that load before the temporary is written, and as its vmcnt model omits LDS-DMA ops, that wait
-  // also covers the previous chunk's operand DMA: one chunk in flight instead of two.
-  int skp[4];  // image pixel of tile pixel 64 pw + 16 i + lane / 4 (DMA round i): the index of a
-               // strided buffer view (stride = the source's channel count x 4 B)
-  int skq;     // byte offset of this lane's swizzled channel quad (see dma)
+  // Skip chunks issue their weight DMA only - no register load, no per-chunk VALU: a dead
+  // placeholder load would free its VGPRs for VALU temporaries, the compiler would then wait (vmcnt)
+  // for it, and as its vmcnt model omits LDS-DMA ops, that wait would also drain the DMA in flight.
   float valid[IT];
   float gmax = 0.f;  // range guard: largest |operand| this thread split
 
@@ -236,16 +235,6 @@ struct XProducer {
     // act == ACT_NONE: the coefficient loads still issue (fixed vmcnt arithmetic) from the input
     ra = p.actA ? mkrsrc(p.actA + ((size_t)t.n0 + pimg) * ctot) : r0;
     rb = p.actB ? mkrsrc(p.actB + ((size_t)t.n0 + pimg) * ctot) : r0;
-    tn0 = t.n0;
-    if (SKIP) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = 64 * (ptid >> 6) + 16 * i + ((ptid & 63) >> 2);
-        const int mi = m / (Geo::TH * TW), mp = m % (Geo::TH * TW);  // image of the tile, its pixel
-        skp[i] = mi * p.H * p.W + (t.y0 + mp / TW) * p.W + t.x0 + mp % TW;
-      }
-      skq = 16 * ((ptid & 3) ^ ((ptid >> 4) & 3));
-    }
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int y = t.y0 + hy[i] - 1, x = t.x0 + hx[i] - 1;
@@ -269,7 +258,7 @@ struct XProducer {
   }
 
   // ism: a 3x3 chunk (idx = its 16-channel chunk of the main input) or a 1x1 skip chunk (idx =
-  // its chunk of the skip input); see KCursor for the order
+  // its 64-channel chunk of the skip input)
   __device__ __forceinline__ void load(Set& s, const ConvParams& p, bool ism, int idx) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) s.vld[i] = valid[i];
@@ -295,36 +284,20 @@ struct XProducer {
     s.cb[1] = bld4(rb, 32 * hh + 16, cb0 * 4);
   }
 
-  // LDS-DMA of chunk c of channel tile ct into ring slot `Wslot` (XDMA3 / XDMA1 ops per thread):
-  //   3x3 chunk: the weight slab (9 rounds of 1 KiB per producer wave);
-  //   skip chunk kk: weights [1][part][h][64][8] (4 KiB, one round) at slot offset 0; the raw fp32
-  //     operand (16 channels = 64 B of each of the tile's 256 pixels, from s0 or s1) pixel-major at
-  //     XSKA, 16 pixels per round (4 lanes per pixel: 16 cache lines per wave-instruction), the
-  //     lane's 16-B quad slot XOR-swizzled by (pixel >> 2) & 3 so the consumers' ds_read_b128 are
-  //     conflict-free.
+  // LDS-DMA of chunk idx of channel tile ct into ring slot `Wslot`: the 3x3 weight slab (XDMA3
+  // rounds of 1 KiB per producer wave) or the 1x1 skip slab (XDMA1 rounds).
   __device__ __forceinline__ void dma(const ConvParams& p, int ct, bool ism, int idx, int nmain, int nskip,
                                       lds_f* Wslot) const {
     if (X3_ABLATE == 5 || X3_ABLATE >= 8) return;
     const int pw = __builtin_amdgcn_readfirstlane(ptid >> 6);
     if (SKIP && !ism) {
-      const int kk = idx;
-      const rsrc_t r = mkrsrc(p.wskip + ((size_t)ct * nskip + kk) * (XW / 9));
-      const int qb = pw * 64;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(Wslot + 4 * qb), 16,
-                                               lane16, 16 * qb, 0, 0);
-      const int cs = 16 * kk;
-      const bool first = cs < p.sc0;
-      const int sc = first ? p.sc0 : p.sc1;
-      // strided view of the source image: record = pixel (sc x 4 B), index skp[i], offset skq
-      const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>((first ? p.s0 : p.s1) + (size_t)tn0 * p.H * p.W * sc), (short)(sc * 4), 0x7ffffff0,
-          0x00020000);
-      const int soff = (first ? cs : cs - p.sc0) * 4;
+      const rsrc_t r = mkrsrc(p.wskip + ((size_t)ct * nskip + idx) * XWS);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_struct_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(Wslot + XSKA + 16 * (64 * pw + 16 * i)), 16, skp[i], skq,
-            soff, 0, 0);
+      for (int i = 0; i < XDMA1; ++i) {
+        const int qb = (i * 4 + pw) * 64;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(Wslot + 4 * qb), 16,
+                                                 lane16, 16 * qb, 0, 0);
+      }
       return;
     }
     // per-lane offset = the loop-invariant 16 * lane (lane16), the round in the scalar offset: a
@@ -457,71 +430,6 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
   }
 }
 
-// One 1x1 skip chunk: the raw fp32 operand (pixel-major [256 px][4 swizzled quads][4] at As) is
-// split in registers with the producers' arithmetic (a_hi = f16(a), a_lo = f16(a - a_hi)), then
-// the 3 split products x 2 x 2 fragment blocks. pb = tile pixel.
-template <int NPROD>
-__device__ __forceinline__ void consume_skip(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws,
-                                             const int (&pb)[2], float& gmax) {
-  const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-  const lds_f* Wb = Ws + 4 * (h * XBN + l32);
-  f16x8 ah[2], al[2], bs[2], bl[2];
-#pragma unroll
-  for (int mr = 0; mr < 2; ++mr) {
-    const int sw = (pb[mr] >> 2) & 3;  // quad Q of pixel m sits in slot Q ^ ((m >> 2) & 3)
-    const f32x4 q0 = *(const lds_f4*)(As + 16 * pb[mr] + 4 * ((2 * h) ^ sw));
-    const f32x4 q1 = *(const lds_f4*)(As + 16 * pb[mr] + 4 * ((2 * h + 1) ^ sw));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float v = j < 4 ? q0[j] : q1[j - 4];
-      gmax = fmaxf(gmax, fabsf(v));  // range guard (the raw residual stream is not normalised)
-      const _Float16 hv = (_Float16)v;
-      ah[mr][j] = hv;
-      al[mr][j] = (_Float16)(v - (float)hv);
-    }
-  }
-#pragma unroll
-  for (int nr = 0; nr < 2; ++nr) {
-    bs[nr] = *(const lds_h8*)(Wb + 4 * (nr * 32));
-    bl[nr] = *(const lds_h8*)(Wb + 4 * (2 * XBN + nr * 32));
-  }
-#pragma unroll
-  for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-    for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(ah[mr], bs[nr], acc[mr][nr]);
-  if (NPROD == 1) return;
-#pragma unroll
-  for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-    for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(ah[mr], bl[nr], acc[mr][nr]);
-#pragma unroll
-  for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-    for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(al[mr], bs[nr], acc[mr][nr]);
-}
-
-// Order of a unit's K stream: the 3x3 chunks, then the 1x1 skip chunks. (Measured alternative,
-// r02: interleaving the skip chunks among the 3x3 chunks in proportion made the skip layers 18 %
-// SLOWER — each 3x3 chunk's prologue VALU, done by the producers one interval ahead, then lands in
-// a short skip interval with no MFMA work to hide behind, once per 3x3 chunk instead of once per
-// unit.)
-struct KCursor {
-  int mi, si;
-  __device__ __forceinline__ void reset() { mi = si = 0; }
-  // kind of the chunk at stream position c (in order, one call per position); idx = its index
-  __device__ __forceinline__ bool next(int c, int S, int nmain, int nskip, int& idx) {
-    if (S > 1) {  // a split-K unit starts mid-stream
-      const bool m = c < nmain;
-      idx = m ? c : c - nmain;
-      return m;
-    }
-    (void)nskip;
-    const bool m = mi < nmain;  // 3x3 chunks first, then the 1x1 skip chunks
-    idx = m ? mi++ : si++;
-    return m;
-  }
-};
-
 template <int XF, bool SKIP, int TW, int NPROD>
 __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   using Geo = XGeo<TW>;
@@ -539,7 +447,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   const int G = gridDim.x;
   const int nu = (nunit - (int)blockIdx.x + G - 1) / G;  // host guarantees >= 1
   const int nmain = p.cin_pad / 16;
-  const int nskip = SKIP ? p.cs_pad / 16 : 0;
+  const int nskip = SKIP ? p.cs_pad / XSK : 0;
   const int nchu = (nmain + nskip) / S;  // chunks per unit (host: divisible)
   const int J = nu * nchu;
   const XDec dec = x3_dec(p, nct);
@@ -549,13 +457,12 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     const int h = lane >> 5, l32 = lane & 31;
     const int wm0 = wave * 64;
     f32x16 acc[2][2];
-    int pb[2], pbs[2];
+    int pb[2];
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr) {
       const int m = wm0 + mr * 32 + l32;
       const int mi = m / (Geo::TH * TW), mp = m % (Geo::TH * TW);  // image of the tile, its pixel
       pb[mr] = mi * Geo::HP + (mp / TW) * Geo::HW + (mp % TW);
-      pbs[mr] = m;
     }
     auto zero = [&]() {
 #pragma unroll
@@ -585,10 +492,12 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     auto vbase = [&](const STile& t) {
       return (((wimg * p.H + t.y0 + wrow) * p.W + t.x0 + 4 * h) * p.cout + t.ct * XBN + l32) * 4;
     };
+    // SKIP kernels have no residual (the host runs a 1x1 conv with a residual, proj_out, split-K: the
+    // reduction adds it). Its 64 registers would not fit beside the skip operand buffers.
     auto prefetch = [&](const STile& t) {
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr) bias2[nr] = gld1(p.bias + t.ct * XBN + 32 * nr + l32);
-      if (!p.res) return;
+      if (SKIP || !p.res) return;
       const rsrc_t rr = mkrsrc(p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout);
       if (p.res_xform == XF_NONE) {
         const int vb = vbase(t);
@@ -639,7 +548,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           for (int r = 0; r < 16; ++r) {
             float x = acc[mr][nr][r] * (1.0f / kLo);  // exact rescale
             x = x + bias2[nr];
-            if (p.res) x = rv[mr][nr][r] + x;  // torch order: x_res + (conv + bias)
+            if (!SKIP && p.res) x = rv[mr][nr][r] + x;  // torch order: x_res + (conv + bias)
             v[mr][r] = x;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep + nr * 128,
                                                   roff(r), 0);
@@ -682,46 +591,172 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         }
       }
     };
+    // ---- 1x1 skip chunks: the lane's operand = channels [XSK/2 h, XSK/2 (h + 1)) of the chunk at tile
+    // pixels wm0 + 32 mr + l32, loaded into registers two chunks ahead. Sub-chunk q (one k = 16 MFMA
+    // step) takes channels XSK/2 h + 8 q + (0..7), quads 2q and 2q+1; the host packs the weights in
+    // the same order (unet.hip pack_skip_x3).
+    f32x4 sq0[2][XSL], sq1[2][XSL];
+    rsrc_t rs0, rs1;
+    int so0[2], so1[2];
+    auto skip_setup = [&](const STile& t) __attribute__((always_inline)) {
+      const size_t img = (size_t)p.H * p.W;
+      rs0 = mkrsrc(p.s0 + (X3_ABLATE == 12 ? 0 : (size_t)t.n0 * img * p.sc0));
+      rs1 = p.s1 ? mkrsrc(p.s1 + (size_t)t.n0 * img * p.sc1) : rs0;
+#pragma unroll
+      for (int mr = 0; mr < 2; ++mr) {
+        const int m = wm0 + mr * 32 + l32;
+        const int mi = m / (Geo::TH * TW), mp = m % (Geo::TH * TW);
+        const int pix = X3_ABLATE == 12 ? m : mi * p.H * p.W + (t.y0 + mp / TW) * p.W + t.x0 + mp % TW;
+        so0[mr] = (pix * p.sc0 + (XSK / 2) * h) * 4;
+        so1[mr] = (pix * p.sc1 + (XSK / 2) * h) * 4;
+      }
+    };
+    auto skip_load = [&](f32x4(&b)[2][XSL], int sk, int q) __attribute__((always_inline)) {  // quads 2q, 2q+1 of skip chunk sk
+      const int cs = XSK * sk;
+      const bool first = cs < p.sc0;
+      const int soff = (first ? cs : cs - p.sc0) * 4 + 32 * q;
+#pragma unroll
+      for (int mr = 0; mr < 2; ++mr) {
+        const int vo = first ? so0[mr] : so1[mr];
+        b[mr][2 * q] = bld4(first ? rs0 : rs1, vo, soff);
+        b[mr][2 * q + 1] = bld4(first ? rs0 : rs1, vo, soff + 16);
+      }
+    };
+    auto skip_load_all = [&](f32x4(&b)[2][XSL], int sk) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < XSQ; ++q) skip_load(b, sk, q);
+    };
+    float gmax = 0.f;
+    // one skip chunk from registers b (weights at Ws: [q][part][h][64 co][8 f16]); with `reload`, sub-chunk
+    // q's quads are reloaded with skip chunk `next` as soon as they are split. `reload` is a constant at
+    // every call site: a run-time test per sub-chunk would make each quad a branch merge of two values.
+    auto skip_chunk = [&](f32x4(&b)[2][XSL], const lds_f* Ws, bool reload, int next) __attribute__((always_inline)) {
+      const lds_f* Wb = Ws + 4 * (h * XBN + l32);
+      f16x8 ah[2], al[2], bs[2], bl[2];
+#pragma unroll
+      for (int q = 0; q < XSQ; ++q) {
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr) {
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = b[mr][2 * q][i];
+            v[4 + i] = b[mr][2 * q + 1][i];
+          }
+          // range guard (the raw residual stream is not normalised)
+          gmax = fmaxf(gmax, fmaxf(fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))),
+                                   fmaxf(fmaxf(fabsf(v[4]), fabsf(v[5])), fmaxf(fabsf(v[6]), fabsf(v[7])))));
+          unsigned hw[4], lw[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (NPROD == 1) {
+              float a0 = v[2 * k], a1 = v[2 * k + 1];
+              asm volatile("" : "+v"(a0), "+v"(a1));
+              hw[k] = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a0, a1}, f16x2));
+            } else {
+              split2(v[2 * k], v[2 * k + 1], hw[k], lw[k]);
+            }
+          }
+          ah[mr] = __builtin_bit_cast(f16x8, u32x4{hw[0], hw[1], hw[2], hw[3]});
+          if (NPROD == 3) al[mr] = __builtin_bit_cast(f16x8, u32x4{lw[0], lw[1], lw[2], lw[3]});
+        }
+        if (reload) skip_load(b, next, q);
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr) {
+          bs[nr] = *(const lds_h8*)(Wb + 4 * (q * 4 * XBN + nr * 32));
+          if (NPROD == 3) bl[nr] = *(const lds_h8*)(Wb + 4 * (q * 4 * XBN + 2 * XBN + nr * 32));
+        }
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(ah[mr], bs[nr], acc[mr][nr]);
+        // one sub-chunk at a time: unconstrained, the scheduler hoists every sub-chunk's split and
+        // fragment reads to the top and the live set no longer fits beside the two operand buffers
+        __builtin_amdgcn_sched_barrier(0);
+        if (NPROD == 1) continue;
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(ah[mr], bl[nr], acc[mr][nr]);
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int nr = 0; nr < 2; ++nr) acc[mr][nr] = xmfma(al[mr], bs[nr], acc[mr][nr]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    auto stamp = [&](int j, int slot = 0) {  // slot 0: chunk start, 16: its MFMAs issued
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
+        p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
+    };
     zero();
     XBARRIER_CONSUMER();  // chunk 0 staged
-    float gmax = 0.f;
-    int kk = 0, u = 0, z = 0;
-    KCursor kc;
-    STile t = unit_of(0, z);
-    for (int j = 0; j < J; ++j) {
-      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
-        p.trace[64 * blockIdx.x + j] = __builtin_amdgcn_s_memtime();
-      const lds_f* Ws = W0 + (j % 3) * XW;
-      const int c = z * nchu + kk;  // chunk position within the tile's K stream
-      if (kk == 0) kc.reset();
-      int cidx;
-      const bool cmain = kc.next(c, S, nmain, nskip, cidx);
-      if (kk == nchu - 1 && S == 1 && X3_ABLATE < 9) prefetch(t);
-      if (X3_ABLATE == 4) {
-      } else if (!SKIP || cmain) {
-        consume_x3<TW, NPROD>(acc, A0 + (j & 1) * XA, Ws, pb);
+    int j = 0;  // position in the block's chunk stream: ring slot j % 3, A stage j & 1
+    for (int u = 0; u < nu; ++u) {
+      int z;
+      const STile t = unit_of(u, z);
+      // the unit's K range [c0, c1): 3x3 chunks [c0, me), then skip chunks [sb, se) of the 1x1 segment
+      const int c0 = z * nchu, c1 = c0 + nchu;
+      const int me = c1 < nmain ? c1 : nmain;
+      const int sb = (c0 > nmain ? c0 : nmain) - nmain, se = c1 - nmain;
+      const bool has_skip = SKIP && sb < se;
+      auto main_chunk = [&]() __attribute__((always_inline)) {
+        stamp(j);
+        if (X3_ABLATE != 4) consume_x3<TW, NPROD>(acc, A0 + (j & 1) * XA, W0 + (j % 3) * XW, pb);
+        stamp(j, 16);
+        ++j;
+        XBARRIER_CONSUMER();
+      };
+      // The unit's last 3x3 chunk is peeled: what it prefetches (residual, first skip operands) is then
+      // not a loop-carried value. The two cases are separate branches so that the operand buffers are
+      // defined on every path to their use (otherwise they would stay live across all 3x3 chunks).
+      if (!has_skip) {
+        for (int c = c0; c < me - 1; ++c) main_chunk();
+        if (me > c0) {
+          if (!SKIP && S == 1) prefetch(t);
+          main_chunk();
+        }
       } else {
-        consume_skip<NPROD>(acc, Ws + XSKA, Ws, pbs, gmax);
+        skip_setup(t);
+        for (int c = c0; c < me - 1; ++c) main_chunk();
+        // one definition point per operand buffer on every path (a buffer defined in two branches
+        // gets register copies at the merge, and a copy of a load in flight is a vmcnt wait)
+        const int sb1 = sb + 1 < se ? sb + 1 : sb;  // (a one-chunk segment reloads its chunk: harmless)
+        skip_load_all(sq0, sb);                      // a whole 3x3 chunk ahead of its use
+        if (me > c0) main_chunk();
+        skip_load_all(sq1, sb1);
+        auto skip_step = [&](f32x4(&b)[2][XSL], bool reload, int next) __attribute__((always_inline)) {
+          stamp(j);
+          skip_chunk(b, W0 + (j % 3) * XW, reload, next);
+          stamp(j, 16);
+          ++j;
+          XBARRIER_CONSUMER();
+        };
+        int sk = sb;
+        for (; sk + 3 < se; sk += 2) {  // pairs whose chunks both have a successor two ahead
+          skip_step(sq0, true, sk + 2);
+          skip_step(sq1, true, sk + 3);
+        }
+        // the last 1 to 3 chunks
+        if (sk + 2 < se) {
+          skip_step(sq0, true, sk + 2);
+          skip_step(sq1, false, 0);
+          skip_step(sq0, false, 0);
+        } else {
+          skip_step(sq0, false, 0);
+          if (sk + 1 < se) skip_step(sq1, false, 0);
+        }
       }
-      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
-        p.trace[64 * blockIdx.x + 16 + j] = __builtin_amdgcn_s_memtime();
-      if (++kk == nchu) {
-        kk = 0;
-        if (X3_ABLATE < 9)
-          epilogue(t, z);
-        else
-          asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
-        zero();
-        if (++u < nu) t = unit_of(u, z);
-      }
-      if (X3_ABLATE != 10) XBARRIER_CONSUMER();
+      if (SKIP && S == 1) prefetch(t);  // (bias only: SKIP kernels have no residual)
+      epilogue(t, z);
+      zero();
     }
     if (SKIP && p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
     return;
   }
 
-  // ---- producers: halo two chunks ahead in registers, weights (and skip operands) two chunks
-  // ahead by LDS-DMA into a 3-slot ring (chunk j in slot j % 3) ----
+  // ---- producers: halo two chunks ahead in registers, weights two chunks ahead by LDS-DMA into a
+  // 3-slot ring (chunk j in slot j % 3) ----
   const int ptid = tid - NP_T;
   XProducer<XF, SKIP, TW, NPROD> P;
   P.init(ptid);
@@ -734,13 +769,12 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   int jl = 0, ul = 0, kl = 0, zl = 0;
   STile tl = unit_of(0, zl);
   int lastmain = 1, prevmain = 1;  // the last / the previous issued chunk is a 3x3 chunk
-  KCursor pc;
   int cmain = 1, cidx = 0;  // kind / index of the cursor's chunk (kept for the clamped repeats)
   auto issue = [&](typename XProducer<XF, SKIP, TW, NPROD>::Set& s) {  // DMA + register loads of the cursor's chunk, then advance
     if (jl < J) {
-      const int c = __builtin_amdgcn_readfirstlane(zl * nchu + kl);
-      if (kl == 0) pc.reset();
-      cmain = pc.next(c, S, nmain, nskip, cidx) ? 1 : 0;
+      const int c = __builtin_amdgcn_readfirstlane(zl * nchu + kl);  // 3x3 chunks, then the skip chunks
+      cmain = c < nmain ? 1 : 0;
+      cidx = cmain ? c : c - nmain;
     }
     prevmain = lastmain;
     lastmain = (!SKIP || cmain) ? 1 : 0;
@@ -758,27 +792,27 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     }
   };
   // Barrier once chunk q's DMA has landed, chunk q+1 being the last issued: younger are chunk q's
-  // register loads (L = Geo::LOADS, none for a skip chunk), then all of chunk q+1 (9 + L, or 5).
-  static_assert(XWDMA == XDMA3 && XDMA1 == 5 && (Geo::LOADS == 10 || Geo::LOADS == 12), "barrier vmcnt literals");
+  // register loads (L = Geo::LOADS, none for a skip chunk), then all of chunk q+1 (9 + L, or XDMA1).
+  static_assert(XWDMA == XDMA3 && XDMA1 == 2 && (Geo::LOADS == 10 || Geo::LOADS == 12), "barrier vmcnt literals");
   auto barrier = [&]() {
     if constexpr (Geo::LOADS == 10) {
       if (!SKIP || (prevmain && lastmain))
         XBARRIER_PRODUCER(29);
       else if (prevmain)
-        XBARRIER_PRODUCER(15);
+        XBARRIER_PRODUCER(12);
       else if (lastmain)
         XBARRIER_PRODUCER(19);
       else
-        XBARRIER_PRODUCER(5);
+        XBARRIER_PRODUCER(2);
     } else {
       if (!SKIP || (prevmain && lastmain))
         XBARRIER_PRODUCER(33);
       else if (prevmain)
-        XBARRIER_PRODUCER(17);
+        XBARRIER_PRODUCER(14);
       else if (lastmain)
         XBARRIER_PRODUCER(21);
       else
-        XBARRIER_PRODUCER(5);
+        XBARRIER_PRODUCER(2);
     }
   };
   issue(s0);  // chunk 0
@@ -786,7 +820,6 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   issue(s1);  // chunk 1
   if (main0) P.store(s0, p.act, A0);  // (a split-K unit may start in the skip segment)
   barrier();
-  if (X3_ABLATE == 10) return;
   // interval j: LDS writes of chunk j+1 (its loads were issued one interval ago), then the DMA and
   // halo loads of chunk j+2, then the barrier once chunk j+1's DMA (issued in interval j-1) has
   // landed. Writes BEFORE issue: hipcc's vmcnt model does not count LDS-DMA ops, so a wait for
@@ -837,21 +870,22 @@ static int launch_x3_tw(const ConvParams& p, int xform, hipStream_t stream) {
 }  // namespace
 
 // Eligible: 3x3, BN = 64, 256-pixel tiles of one image (8 x 32 or 16 x 16), NHWC epilogue, cout a
-// multiple of 64, 16-channel chunks on every source (main and skip; skip sources < 4096 channels: the
-// strided view's 14-bit stride), K chunks divisible by the
-// split, no avg-pool prologue (run_conv feeds those layers a pooled activation instead) nor
+// multiple of 64, 16-channel chunks on the main sources and 64-channel chunks on the skip sources,
+// K chunks divisible by the split, no avg-pool prologue (run_conv feeds those layers a pooled activation instead) nor
 // avg-pool residual without split-K (pooled likewise). Any act, identity or nearest-up residual,
 // 1x1 skip segment.
 bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
-  const int nch = p.cin_pad / 16 + (p.wskip ? p.cs_pad / 16 : 0);
+  const int nch = p.cin_pad / 16 + (p.wskip ? p.cs_pad / XSK : 0);
   const bool one_img = (p.TW == 32 || p.TW == 16) && p.TH * p.TW == 256 && p.IMGS == 1;
   const bool img8 = p.TW == 8 && p.TH == 8 && p.H == 8 && p.W == 8 && p.IMGS == 4 && p.N % 4 == 0 && !p.opt_invariant &&
                     xform == XF_NONE && (!p.res || p.res_xform == XF_NONE);
   const bool only1x1 = taps == 1 && p.cin_pad == 0 && p.wskip;  // a 1x1 conv: 1x1 chunks only
   return (taps == 9 || only1x1) && xform != XF_DOWN && bn == XBN && p.bm == 256 && (one_img || img8) &&
          p.epi == EPI_NHWC && p.cout % XBN == 0 && p.cout_pad == p.cout &&
-         p.c0 % 16 == 0 && p.c1 % 16 == 0 && (!p.wskip || (p.sc0 % 16 == 0 && p.sc1 % 16 == 0 && p.sc0 < 4096 && p.sc1 < 4096)) &&
-         p.ksplit >= 1 && nch % p.ksplit == 0 && (!p.res || p.res_xform != XF_DOWN || p.ksplit > 1);
+         p.c0 % 16 == 0 && p.c1 % 16 == 0 &&
+         (!p.wskip || (p.sc0 % XSK == 0 && p.sc1 % XSK == 0 && p.cs_pad == p.sc0 + p.sc1)) &&
+         p.ksplit >= 1 && nch % p.ksplit == 0 && (!p.res || p.res_xform != XF_DOWN || p.ksplit > 1) &&
+         (!p.wskip || !p.res || p.ksplit > 1);  // a SKIP kernel's residual goes through the split-K reduction
 }
 
 int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream) {

@@ -160,7 +160,9 @@ class Model {
   int opt_bm128_ = 0;       // 128-pixel fp32 tiles only
   int opt_lds_pad_ = 0;     // extra LDS bytes per fp32 conv block
   int opt_invariant_ = 0;   // batch-invariant geometry (results independent of the batch split)
+  int opt_x3_order_ = 0;    // split kernel unit order (ConvParams::opt_x3_order)
   void fill_opts(ConvParams& p) const {
+    p.opt_x3_order = opt_x3_order_;
     p.opt_bm128 = opt_bm128_;
     p.opt_lds_pad = opt_lds_pad_;
     p.opt_stream_cw = opt_stream_cw_;

@@ -32,6 +32,7 @@ Model::Model(const ifd_config& cfg) : cfg_(cfg) {
   opt_bm128_ = env_int("IFD_CONV_BM", 0) == 128;
   opt_lds_pad_ = env_int("IFD_CONV_LDS_PAD", 0);
   opt_invariant_ = env_int("IFD_BATCH_INVARIANT", 0) != 0;
+  opt_x3_order_ = env_int("IFD_X3_ORDER", 0);
 }
 
 int Model::set_option(const std::string& key, int v) {
@@ -50,6 +51,9 @@ int Model::set_option(const std::string& key, int v) {
   } else if (key == "lds_pad") {
     IFD_REQUIRE(v >= 0 && v <= 65536, "lds_pad out of range");
     opt_lds_pad_ = v;
+  } else if (key == "x3_order") {
+    IFD_REQUIRE(v >= 0 && v <= 2, "x3_order must be 0, 1 or 2");
+    opt_x3_order_ = v;
   } else if (key == "batch_invariant") {
     if ((v != 0) != (opt_invariant_ != 0)) ws_B_ = 0;  // split-K slab sizing depends on it: re-plan
     opt_invariant_ = v != 0;
@@ -67,6 +71,7 @@ int Model::get_option(const std::string& key, int* v) const {
   else if (key == "conv_bm128") *v = opt_bm128_;
   else if (key == "lds_pad") *v = opt_lds_pad_;
   else if (key == "batch_invariant") *v = opt_invariant_;
+  else if (key == "x3_order") *v = opt_x3_order_;
   else IFD_REQUIRE(false, "unknown option " + key);
   return 0;
 }
@@ -370,6 +375,48 @@ static bool pack_conv_x3(const std::vector<float>& w, int cout, int cin, int tap
   return ok;
 }
 
+// 3xf16 1x1 skip packing in kSkipChunk-channel chunks (conv_x3.hip skip_chunk): [Cout_pad/BN][Cs_pad/K][q]
+// [part][h][BN][8] f16, element (q, part, h, col, j) of (ct, chunk s) = split part of
+// W[ct*BN + col][K s + K/2 h + 8 q + j] (the consumer lane of channel half h holds channels K/2 h ..
+// K/2 (h + 1) - 1 of the chunk; sub-chunk q of the k = 16 MFMA step takes 8 of them). Same parts and
+// range check as pack_conv_x3.
+static constexpr int kSkipChunk = 32;
+static bool pack_skip_x3(const std::vector<float>& w, int cout, int cin, int bn, int cs_pad, int cout_pad,
+                         std::vector<float>& blob, size_t off) {
+  constexpr int K = kSkipChunk, NQ = K / 16;
+  const int ns = cs_pad / K;
+  _Float16* dst = reinterpret_cast<_Float16*>(blob.data() + off);
+  bool ok = true;
+  for (int ct = 0; ct < cout_pad / bn; ++ct)
+    for (int sk = 0; sk < ns; ++sk)
+      for (int q = 0; q < NQ; ++q)
+        for (int part = 0; part < 2; ++part)
+          for (int hh = 0; hh < 2; ++hh)
+            for (int col = 0; col < bn; ++col)
+              for (int j = 0; j < 8; ++j) {
+                const int co = ct * bn + col, ci = sk * K + hh * (K / 2) + q * 8 + j;
+                const float v = (co < cout && ci < cin) ? w[(size_t)co * cin + ci] : 0.f;
+                const _Float16 hi = (_Float16)v;
+                _Float16 o;
+                if (part == 0) {
+                  const float sc = (float)hi * 2048.0f;
+                  if (!(std::fabs(sc) <= 65504.0f)) ok = false;
+                  o = (_Float16)sc;
+                } else {
+                  o = (_Float16)((v - (float)hi) * 2048.0f);
+                }
+                dst[((((((size_t)ct * ns + sk) * NQ + q) * 2 + part) * 2 + hh) * bn + col) * 8 + j] = o;
+              }
+  return ok;
+}
+
+// K chunks of a conv on the split kernel: 16-channel 3x3 chunks + kSkipChunk-channel 1x1 skip chunks; a
+// plain 1x1 conv (attention qkv / proj_out) runs as skip chunks only
+static int x3_nchunks(const ConvW& cw) {
+  if (cw.taps == 1 && !cw.has_skip) return cw.cin_pad / kSkipChunk;
+  return cw.cin_pad / 16 + (cw.has_skip ? cw.cs_pad / kSkipChunk : 0);
+}
+
 int Model::guard_reset(hipStream_t s) {
   if (!guard_) {
     IFD_CHECK_HIP(hipMalloc(&guard_, 64));
@@ -410,10 +457,10 @@ int Model::finalize() {
     if (c.has_skip) c.ws_off = reserve((size_t)c.cout_pad * c.cs_pad);
     // 3xf16 packing (two f16 parts = one float slot per weight) for the layers conv_x3 can run
     c.x3_off = c.x3s_off = 0;
-    if (c.taps == 9 && c.bn == 64 && c.cin_pad % 16 == 0 && (!c.has_skip || c.cs_pad % 16 == 0)) {
+    if (c.taps == 9 && c.bn == 64 && c.cin_pad % 16 == 0 && (!c.has_skip || c.cs_pad % kSkipChunk == 0)) {
       c.x3_off = reserve((size_t)c.cout_pad * c.cin_pad * c.taps);
       if (c.has_skip) c.x3s_off = reserve((size_t)c.cout_pad * c.cs_pad);
-    } else if (c.taps == 1 && c.bn == 64 && c.cin_pad % 16 == 0 && !c.has_skip) {
+    } else if (c.taps == 1 && c.bn == 64 && c.cin_pad % kSkipChunk == 0 && !c.has_skip) {
       c.x3s_off = reserve((size_t)c.cout_pad * c.cin_pad);  // a 1x1 conv runs as 1x1 chunks only
     }
   };
@@ -454,9 +501,9 @@ int Model::finalize() {
     c.x3_ok = c.x3_off && pack_conv_x3(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob,
                                        c.x3_off);
     if (c.taps == 1 && c.x3s_off)
-      c.x3_ok = pack_conv_x3(host_[c.wname], c.cout, c.cin, 1, c.bn, c.cin_pad, c.cout_pad, blob, c.x3s_off);
+      c.x3_ok = pack_skip_x3(host_[c.wname], c.cout, c.cin, c.bn, c.cin_pad, c.cout_pad, blob, c.x3s_off);
     if (c.x3_ok && c.has_skip)
-      c.x3_ok = pack_conv_x3(host_[c.swname], c.cout, c.cs, 1, c.bn, c.cs_pad, c.cout_pad, blob, c.x3s_off);
+      c.x3_ok = pack_skip_x3(host_[c.swname], c.cout, c.cs, c.bn, c.cs_pad, c.cout_pad, blob, c.x3s_off);
     const auto& b = host_[c.bname];
     for (int i = 0; i < c.cout; ++i) blob[c.b_off + i] = b[i];
     if (c.has_skip) {
@@ -581,8 +628,9 @@ int Model::ensure_workspace(int B) {
       std::memset(&g, 0, sizeof(g));
       fill_opts(g);
       g.cout_pad = cw.cout_pad;
-      const int nch = x3 ? (cw.cin_pad + (cw.has_skip ? cw.cs_pad : 0)) / 16 : cw.cin_pad / 8;
+      const int nch = x3 ? x3_nchunks(cw) : cw.cin_pad / 8;
       conv_geometry(g, H, H, B, cw.bn, nch, x3 == 1);
+      if (x3 && cw.taps == 1 && !cw.has_skip && g.ksplit == 1 && nch % 2 == 0) g.ksplit = 2;  // see run_conv
       if (g.ksplit > 1) split_floats_ = std::max(split_floats_, (size_t)g.ksplit * B * H * H * cw.cout);
     }
   };
@@ -665,7 +713,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   IFD_REQUIRE((H & (H - 1)) == 0, "spatial size must be a power of two");
   // the persistent split kernel: 256-pixel tiles, K split over units at low resolution
   const bool x3_geo = split_ && cw.x3_ok && epi == EPI_NHWC;
-  const int x3_chunks = (cw.cin_pad + (cw.has_skip ? cw.cs_pad : 0)) / 16;
+  const int x3_chunks = x3_nchunks(cw);
   conv_geometry(p, H, H, N, cw.bn, x3_geo ? x3_chunks : cw.cin_pad / 8, x3_geo);
   if (epi != EPI_NHWC) p.ksplit = 1;
   p.part = ws_ + o_split_;
@@ -695,6 +743,8 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     q.in0 = nullptr; q.c0 = 0; q.in1 = nullptr; q.c1 = 0; q.cin_pad = 0; q.act = ACT_NONE;
     q.s0 = act != ACT_NONE ? ws_ + o_pool_ : in0; q.sc0 = c0; q.s1 = nullptr; q.sc1 = 0;
     q.wskip = wblob_ + cw.x3s_off; q.cs_pad = cw.cin_pad;
+    // a residual (proj_out) is added by the split-K reduction: the split kernel's 1x1 path has none
+    if (q.res && q.ksplit == 1 && x3_chunks % 2 == 0 && 2 * (size_t)N * H * H * cw.cout <= split_floats_) q.ksplit = 2;
     if (conv_x3_eligible(q, 1, XF_NONE, cw.bn)) {
       if (act != ACT_NONE) {
         IFD_REQUIRE((size_t)N * H * H * c0 <= pool_floats_, "act_apply workspace");
