@@ -45,6 +45,7 @@
 //   2 producers load the halo but skip the prologue / split / LDS writes
 //   4 consumers skip the 3x3 MFMAs        5 no weight DMA
 //   8 producers idle (no DMA, no halo)   12 skip operands all read from one tile (cache-resident)
+//   13 no epilogue (accumulators discarded)   14 epilogue without stores   15 epilogue without GN statistics
 #ifndef X3_ABLATE
 #define X3_ABLATE 0
 #endif
@@ -523,7 +524,11 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
             }
       }
     };
-    auto epilogue = [&](const STile& t, int z) {
+    auto epilogue = [&](const STile& t, int z, bool tstamp = false) {
+      if (X3_ABLATE == 13) {  // timing only: no epilogue
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
+        return;
+      }
       const size_t img = (size_t)p.H * p.W * p.cout;
       const int vb = vbase(t);
       if (S > 1) {  // raw partial sums into slab z (splitk_reduce adds the slabs, bias, residual)
@@ -539,9 +544,9 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         return;
       }
       const rsrc_t ro = mkrsrc(p.out + (size_t)t.n0 * img);
+      // the outputs replace the accumulators (they are zeroed after the epilogue)
 #pragma unroll
-      for (int nr = 0; nr < 2; ++nr) {
-        float v[2][16];
+      for (int nr = 0; nr < 2; ++nr)
 #pragma unroll
         for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
@@ -549,47 +554,86 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
             float x = acc[mr][nr][r] * (1.0f / kLo);  // exact rescale
             x = x + bias2[nr];
             if (!SKIP && p.res) x = rv[mr][nr][r] + x;  // torch order: x_res + (conv + bias)
-            v[mr][r] = x;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep + nr * 128,
-                                                  roff(r), 0);
+            acc[mr][nr][r] = x;
+            if (X3_ABLATE != 14)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep + nr * 128,
+                                                    roff(r), 0);
           }
-        if (p.gstat) {
-          // GroupNorm granule statistics: channel over this lane's 32 pixels (two-pass), merged
-          // with the other column half (lane ^ 32), then over the channel quad (lanes ^ 1, ^ 2)
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
+        p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values + stores issued
+      if (X3_ABLATE != 15 && p.gstat) {
+        // GroupNorm granule statistics of each output channel: over this lane's 32 pixels (two-pass),
+        // then merged with the other column half (lane ^ 32) and over the channel quad (lanes ^ 1,
+        // ^ 2). Every merge joins two equal counts, so Chan's update needs no division:
+        //   mean = ma + d / 2,  M2 = (M2a + M2b) + d^2 n / 2,  d = mb - ma  (n = one side's count)
+        // (bit-identical to gmerge: the factors are powers of two). The partner values come from
+        // v_permlane32_swap and DPP quad permutes (VALU) instead of LDS-routed shuffles, and the two
+        // channel blocks' chains are interleaved.
+        float mean[2], m2[2];
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr) {
           float sm = 0.f;
 #pragma unroll
           for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sm += v[mr][r];
-          const float mean = sm * (1.0f / 32);
-          float m2 = 0.f;
+            for (int r = 0; r < 16; ++r) sm += acc[mr][nr][r];
+          mean[nr] = sm * (1.0f / 32);
+          float q = 0.f;
 #pragma unroll
           for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const float d = v[mr][r] - mean;
-              m2 += d * d;
+              const float d = acc[mr][nr][r] - mean[nr];
+              q += d * d;
             }
-          GStat g = {32.f, mean, m2};
-          auto xmerge = [&](GStat a, int off) {
-            GStat b;
-            b.n = __shfl_xor(a.n, off);
-            b.mean = __shfl_xor(a.mean, off);
-            b.m2 = __shfl_xor(a.m2, off);
-            return (lane & off) == 0 ? gmerge(a, b) : gmerge(b, a);
-          };
-          g = xmerge(g, 32);
-          g = xmerge(g, 1);
-          g = xmerge(g, 2);
-          if (h == 0 && (l32 & 3) == 0) {
-            const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
+          m2[nr] = q;
+        }
+        auto merge = [&](float am, float aq, float bm, float bq, float n, float& om, float& oq) {
+          const float d = bm - am;
+          om = am + d * 0.5f;
+          oq = (aq + bq) + ((d * d) * n) * 0.5f;
+        };
+        // lane ^ 32: v_permlane32_swap of a value with a copy of itself leaves, in every lane, the lower
+        // half's value in the first register and the upper half's in the second. (Inline asm with the
+        // copy inside: the builtin, and a two-result asm returned through a vector, both came out of
+        // hipcc reading the first register for both results.)
+        auto swap32 = [](float v, float& lo, float& hi) {
+          unsigned a = __builtin_bit_cast(unsigned, v), b;
+          asm volatile("v_mov_b32 %1, %0\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "=&v"(b));
+          lo = __builtin_bit_cast(float, a);
+          hi = __builtin_bit_cast(float, b);
+        };
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr) {
+          float ml, mh, ql, qh;
+          swap32(mean[nr], ml, mh);
+          swap32(m2[nr], ql, qh);
+          merge(ml, ql, mh, qh, 32.f, mean[nr], m2[nr]);
+        }
+        // lanes ^ 1 then ^ 2 within the quad: quad_perm [0,0,2,2] / [1,1,3,3], then [0,1,0,1] / [2,3,2,3]
+#define IFD_QP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false))
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+          merge(IFD_QP(mean[nr], 0xA0), IFD_QP(m2[nr], 0xA0), IFD_QP(mean[nr], 0xF5), IFD_QP(m2[nr], 0xF5), 64.f, mean[nr],
+                m2[nr]);
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+          merge(IFD_QP(mean[nr], 0x44), IFD_QP(m2[nr], 0x44), IFD_QP(mean[nr], 0xEE), IFD_QP(m2[nr], 0xEE), 128.f, mean[nr],
+                m2[nr]);
+#undef IFD_QP
+        if (h == 0 && (l32 & 3) == 0) {
+          const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
+#pragma unroll
+          for (int nr = 0; nr < 2; ++nr) {
             float* o = p.gstat + (((size_t)(t.n0 + wimg) * (p.cout / 4) + t.ct * 16 + nr * 8 + (l32 >> 2)) *
                                       p.gstat_E + e) * 2;
-            o[0] = g.mean;
-            o[1] = g.m2;
+            o[0] = mean[nr];
+            o[1] = m2[nr];
           }
         }
       }
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
+        p.trace[64 * blockIdx.x + 45] = __builtin_amdgcn_s_memtime();  // statistics done
     };
     // ---- 1x1 skip chunks: the lane's operand = channels [XSK/2 h, XSK/2 (h + 1)) of the chunk at tile
     // pixels wm0 + 32 mr + l32, loaded into registers two chunks ahead. Sub-chunk q (one k = 16 MFMA
@@ -748,7 +792,13 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         }
       }
       if (SKIP && S == 1) prefetch(t);  // (bias only: SKIP kernels have no residual)
-      epilogue(t, z);
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
+        p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
+      epilogue(t, z, u == 0);
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0) {
+        __builtin_amdgcn_s_waitcnt(0);  // (trace builds: wait for the stores to leave)
+        p.trace[64 * blockIdx.x + 63] = __builtin_amdgcn_s_memtime();    // first epilogue: end
+      }
       zero();
     }
     if (SKIP && p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
@@ -825,7 +875,8 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   // landed. Writes BEFORE issue: hipcc's vmcnt model does not count LDS-DMA ops, so a wait for
   // chunk j+1's registers placed after chunk j+2's DMA would also wait for that DMA.
   auto stamp = [&](int slot, int j) {
-    if (IFD_TRACE && p.trace && ptid == 0 && j < 16) p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
+    // (slots of j >= 11 hold the consumer's first-epilogue stamps)
+    if (IFD_TRACE && p.trace && ptid == 0 && j < 11) p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
   };
   for (int j = 0; j < J; j += 2) {
     if (j + 1 < J && lastmain) P.store(s1, p.act, A0 + XA);  // last issued = chunk j+1

@@ -34,3 +34,6 @@ print("consumer issue (start -> MFMAs issued):", med(ce - cs))
 print("producer: interval start -> DMA+loads issued:", med(pi[:, 1:] - cs[:, 1:]))
 print("producer: loads issued -> LDS writes done:", med(ps - pi))
 print("producer: LDS writes done -> next consumer start:", med(cs[:, 1:] - ps[:, :-1]))
+print("first epilogue: start after chunk 0 start", int(np.median(blk[:, 43] - cs[:, 0])),
+      "; phases from its start (values + stores issued, statistics, stores drained):",
+      [int(np.median(blk[:, k] - blk[:, 43])) for k in (44, 45, 63)])
