@@ -263,7 +263,7 @@ struct XProducer {
   __device__ __forceinline__ void load(Set& s, const ConvParams& p, bool ism, int idx) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) s.vld[i] = valid[i];
-    if (X3_ABLATE == 1 || X3_ABLATE >= 8) return;
+    if (X3_ABLATE == 1 || X3_ABLATE == 8) return;
     if (SKIP && !ism) return;  // operand by DMA (see dma)
     const int cb0 = 16 * idx;
     if (cb0 < p.c0) {
@@ -289,7 +289,7 @@ struct XProducer {
   // rounds of 1 KiB per producer wave) or the 1x1 skip slab (XDMA1 rounds).
   __device__ __forceinline__ void dma(const ConvParams& p, int ct, bool ism, int idx, int nmain, int nskip,
                                       lds_f* Wslot) const {
-    if (X3_ABLATE == 5 || X3_ABLATE >= 8) return;
+    if (X3_ABLATE == 5 || X3_ABLATE == 8) return;
     const int pw = __builtin_amdgcn_readfirstlane(ptid >> 6);
     if (SKIP && !ism) {
       const rsrc_t r = mkrsrc(p.wskip + ((size_t)ct * nskip + idx) * XWS);
@@ -335,7 +335,7 @@ struct XProducer {
   }
   template <int ACT>
   __device__ __forceinline__ void store_act(const Set& s, lds_f* As) {
-    if (X3_ABLATE == 1 || X3_ABLATE == 2 || X3_ABLATE >= 8) return;
+    if (X3_ABLATE == 1 || X3_ABLATE == 2 || X3_ABLATE == 8) return;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       if (ldso[i] >= 0) {
@@ -375,6 +375,18 @@ struct XProducer {
     }
   }
 };
+
+// The lower and the upper wave half's value of v, in every lane (the lane ^ 32 exchange of the
+// GroupNorm merges), by two v_permlane32_swap against zero: [v_lo, 0] | [0, v_lo] and [v_hi, 0] |
+// [0, v_hi]. (hipcc miscompiles the builtin given the same value twice: both results come back in
+// one register.)
+__device__ __forceinline__ void wave_halves(float v, float& lo, float& hi) {
+  const unsigned x = __builtin_bit_cast(unsigned, v);
+  const auto a = __builtin_amdgcn_permlane32_swap(x, 0u, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(0u, x, false, false);
+  lo = __builtin_bit_cast(float, a[0] | b[0]);
+  hi = __builtin_bit_cast(float, a[1] | b[1]);
+}
 
 __device__ __forceinline__ f32x16 xmfma(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -593,21 +605,11 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           om = am + d * 0.5f;
           oq = (aq + bq) + ((d * d) * n) * 0.5f;
         };
-        // lane ^ 32: v_permlane32_swap of a value with a copy of itself leaves, in every lane, the lower
-        // half's value in the first register and the upper half's in the second. (Inline asm with the
-        // copy inside: the builtin, and a two-result asm returned through a vector, both came out of
-        // hipcc reading the first register for both results.)
-        auto swap32 = [](float v, float& lo, float& hi) {
-          unsigned a = __builtin_bit_cast(unsigned, v), b;
-          asm volatile("v_mov_b32 %1, %0\n\ts_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "=&v"(b));
-          lo = __builtin_bit_cast(float, a);
-          hi = __builtin_bit_cast(float, b);
-        };
 #pragma unroll
-        for (int nr = 0; nr < 2; ++nr) {
+        for (int nr = 0; nr < 2; ++nr) {  // lane ^ 32
           float ml, mh, ql, qh;
-          swap32(mean[nr], ml, mh);
-          swap32(m2[nr], ql, qh);
+          wave_halves(mean[nr], ml, mh);
+          wave_halves(m2[nr], ql, qh);
           merge(ml, ql, mh, qh, 32.f, mean[nr], m2[nr]);
         }
         // lanes ^ 1 then ^ 2 within the quad: quad_perm [0,0,2,2] / [1,1,3,3], then [0,1,0,1] / [2,3,2,3]
