@@ -159,6 +159,156 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
   }
 }
 
+// Weight gradient, all taps of a 64 co x 64 ci tile per block (v_mfma_f32_32x32x2f32):
+//   dW[co][ci][tap] = sum over output pixels p of dY[p][co] X[p + offset(tap)][ci]
+// K = output pixels in chunks of 32: a 32-pixel row segment, or 32 / W whole rows when W < 32. Per
+// chunk the block stages dY [32 px][64 co] and the X halo [(R + 2) rows][(Wc + 2) cols][64 ci] in LDS
+// pixel-major and channel-contiguous (straight 16-B copies, no transpose), double-buffered: the
+// next chunk's loads are in registers while this chunk's MFMAs run. Wave w owns the 32 x 32
+// quadrant (co 32 (w & 1), ci 32 (w >> 1)) of every tap: TAPS x 16 accumulator registers. Per k pair
+// (chunk pixels j and j + 16, one per lane half) one LDS read of dY serves all taps, and each tap
+// reads X at its shift. The halo makes each X value serve 9 taps (the one-tap-per-block kernel,
+// wgrad_kernel, re-read dY and X per tap at 61 TFLOP/s).
+constexpr int W9_LDS = 32 * 64 + 3 * 34 * 64;  // floats per stage: dY + the largest halo (W >= 32)
+template <int TAPS>
+__global__ __launch_bounds__(256) void wgrad9_kernel(WgArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[2][W9_LDS];
+  const int cin = a.c0 + a.c1;
+  const int nci = (cin + 63) / 64;
+  const int cit = blockIdx.x % nci, cot = blockIdx.x / nci;
+  const int co0 = cot * 64, ci0 = cit * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int wr = 32 * (wave & 1), wc = 32 * (wave >> 1);
+  const int Wc = a.W < 32 ? a.W : 32, R = 32 / Wc;       // chunk: R rows of Wc pixels
+  const int HWc = Wc + 2, HP = (R + 2) * HWc;            // halo row length, halo pixels
+  const int segs = a.W / Wc, rows_per_img = a.H / R;      // chunks per image row block / per image
+  const int64_t nch = (int64_t)a.N * rows_per_img * segs;
+  const int64_t c_beg = (int64_t)blockIdx.y * a.chunks_per_split;
+  const int64_t c_end = c_beg + a.chunks_per_split < nch ? c_beg + a.chunks_per_split : nch;
+  f32x16 acc[TAPS];
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  if (c_beg >= c_end) return;  // (never for the host's split choice)
+
+  // staging items: dY 512 quads (2 per thread), halo HP x 16 quads (<= 7 per thread); the items'
+  // positions within the chunk are fixed per thread (no divisions in the chunk loop)
+  constexpr int XI = 7;
+  f32x4 dyv[2], xv[XI];
+  const int lwc = __builtin_ctz(Wc);
+  int dyo[2], xr[XI], xc[XI];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int px = (tid + 256 * k) >> 4;
+    dyo[k] = (px >> lwc) * a.W + (px & (Wc - 1));  // pixel offset from the chunk origin
+  }
+#pragma unroll
+  for (int k = 0; k < XI; ++k) {
+    const int hp = (tid + 256 * k) >> 4;
+    xr[k] = hp < HP ? hp / HWc - 1 : -1000000;  // halo row / column relative to the chunk origin
+    xc[k] = hp % HWc - 1;
+  }
+  auto chunk_origin = [&](int64_t c, int& n, int& y0, int& x0) {
+    const int64_t per_img = (int64_t)rows_per_img * segs;
+    n = (int)(c / per_img);
+    const int rem = (int)(c - (int64_t)n * per_img);
+    y0 = (rem / segs) * R;
+    x0 = (rem % segs) * Wc;
+  };
+  auto load = [&](int64_t c) {
+    int n, y0, x0;
+    chunk_origin(c, n, y0, x0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k, co = co0 + 4 * (i & 15);
+      const int64_t pix = ((int64_t)n * a.H + y0) * a.W + x0 + dyo[k];
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (co + 3 < a.cout) {
+        v = *reinterpret_cast<const f32x4*>(a.dy + pix * a.cout + co);
+      } else {
+        for (int j = 0; j < 4; ++j)
+          if (co + j < a.cout) v[j] = a.dy[pix * a.cout + co + j];
+      }
+      dyv[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + 256 * k, ci = ci0 + 4 * (i & 15);
+      const int y = y0 + xr[k], x = x0 + xc[k];
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (y >= 0 && y < a.H && x >= 0 && x < a.W && ci < cin) {
+        const int64_t sp = ((int64_t)n * a.H + y) * a.W + x;
+        v = ci < a.c0 ? *reinterpret_cast<const f32x4*>(a.x0 + sp * a.c0 + ci)
+                      : *reinterpret_cast<const f32x4*>(a.x1 + sp * a.c1 + (ci - a.c0));
+      }
+      xv[k] = v;
+    }
+  };
+  auto store = [&](float* L) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k;
+      *reinterpret_cast<f32x4*>(L + (i >> 4) * 64 + 4 * (i & 15)) = dyv[k];
+    }
+    float* X = L + 32 * 64;
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + 256 * k;
+      if ((i >> 4) < HP) *reinterpret_cast<f32x4*>(X + (i >> 4) * 64 + 4 * (i & 15)) = xv[k];
+    }
+  };
+  load(c_beg);
+  for (int64_t c = c_beg; c < c_end; ++c) {
+    float* L = lds[c & 1];
+    store(L);
+    __syncthreads();  // (the other buffer's readers passed this barrier after their previous chunk)
+    if (c + 1 < c_end) load(c + 1);
+    const float* D = L;
+    const float* X = L + 32 * 64;
+    // software-pipelined one k pair ahead: the next pair's LDS reads (1 dY + TAPS X values) are
+    // issued before this pair's MFMAs (left to itself, hipcc waited on each read before its MFMA)
+    float av[2], bv[2][TAPS];
+    auto fetch = [&](int j, int slot) {
+      const int m = j + 16 * h;  // this lane half's pixel of the k pair
+      av[slot] = D[m * 64 + wr + l32];
+      const int hp0 = (m >> lwc) * HWc + (m & (Wc - 1));  // halo pixel of tap (ky, kx) = hp0 + ky HWc + kx
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) {
+        const int ky = TAPS == 9 ? t / 3 : 1, kx = TAPS == 9 ? t % 3 : 1;
+        bv[slot][t] = X[(hp0 + ky * HWc + kx) * 64 + wc + l32];
+      }
+    };
+    // (the next pair's reads go out after this pair's first MFMAs: LDS reads in flight stay within
+    // the 15 lgkmcnt can track, beyond which the wave stalls at issue)
+    constexpr int TH = TAPS > 1 ? TAPS / 2 + 1 : 1;
+    fetch(0, 0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int cur = j & 1;
+#pragma unroll
+      for (int t = 0; t < TH; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur], bv[cur][t], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + 1 < 16) fetch(j + 1, cur ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = TH; t < TAPS; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur], bv[cur][t], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin][taps]
+  float* slab = a.part + (size_t)blockIdx.y * a.cout * cin * TAPS;
+  const int ci = ci0 + wc + l32;
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wr + 8 * (r >> 2) + 4 * h + (r & 3);
+      if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * TAPS + t] = acc[t][r];
+    }
+}
+
 __global__ void slab_reduce_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out,
                                    int accumulate) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -818,11 +968,12 @@ int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, 
   return e;
 }
 
+// split-K count of wgrad9_kernel: blocks (tiles x splits) >= ~2 per CU, >= 8 chunks per split
 int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* splits) {
-  const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64) * taps;
-  const int64_t nch = (P + WG_CH - 1) / WG_CH;
+  const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64);
+  const int64_t nch = P / 32;
   int S = 1;
-  while (S < 256 && (int64_t)tiles * S < 1024 && nch / (2 * S) >= 8) S *= 2;
+  while (S < 1024 && (int64_t)tiles * S < 512 && nch / (2 * S) >= 8) S *= 2;
   if (splits) *splits = S;
   return (int64_t)S * cout * cin * taps;
 }
@@ -841,12 +992,22 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
   WgArgs a;
   a.dy = dy; a.cout = cout; a.x0 = x0; a.c0 = c0; a.x1 = c1 ? x1 : x0; a.c1 = c1;
   a.N = N; a.H = H; a.W = H; a.taps = taps; a.P = P;
-  const int64_t nch = (P + WG_CH - 1) / WG_CH;
-  a.chunks_per_split = (int)((nch + S - 1) / S);
   a.part = part;
-  const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64) * taps;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, S), dim3(256), 0, s, a);
+  if (H >= 8 && (H & (H - 1)) == 0 && (!c1 || c0 % 4 == 0)) {  // wgrad9's chunking: power-of-two sizes >= 8
+    const int64_t nch = P / 32;
+    a.chunks_per_split = (int)((nch + S - 1) / S);
+    const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64);
+    if (taps == 9)
+      hipLaunchKernelGGL(wgrad9_kernel<9>, dim3(tiles, S), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(wgrad9_kernel<1>, dim3(tiles, S), dim3(256), 0, s, a);
+  } else {  // small maps: one tap per block (same split count; its slabs hold fewer used chunks)
+    const int64_t nch = (P + WG_CH - 1) / WG_CH;
+    a.chunks_per_split = (int)((nch + S - 1) / S);
+    const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64) * taps;
+    hipLaunchKernelGGL(wgrad_kernel, dim3(tiles, S), dim3(256), 0, s, a);
+  }
   const int64_t n = (int64_t)cout * cin * taps;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (db) {
