@@ -174,6 +174,9 @@ __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int
   return t;
 }
 
+#ifndef X3_PREF
+#define X3_PREF 2
+#endif
 #ifndef X3_PINF
 #define X3_PINF 1
 #endif
@@ -757,10 +760,12 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       // not a loop-carried value. The two cases are separate branches so that the operand buffers are
       // defined on every path to their use (otherwise they would stay live across all 3x3 chunks).
       if (!has_skip) {
-        for (int c = c0; c < me - 1; ++c) main_chunk();
+        // the residual / bias prefetch goes out X3_PREF chunks before the unit's end (peeled)
+        constexpr int PF = X3_PREF;
+        for (int c = c0; c < me - PF; ++c) main_chunk();
         if (me > c0) {
           if (!SKIP && S == 1) prefetch(t);
-          main_chunk();
+          for (int c = (me - PF > c0 ? me - PF : c0); c < me; ++c) main_chunk();
         }
       } else {
         skip_setup(t);
