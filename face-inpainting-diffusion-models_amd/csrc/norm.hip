@@ -284,42 +284,62 @@ __device__ __forceinline__ double block_sum64(double v, double* sh) {
   return s;
 }
 
-// one block per (group g, image n). Every entry of a source holds `cnt` values (mean, M2), so the
-// group statistics are two fp64 passes over the group's entries (all granules, both concat
-// sources): mean = sum(cnt * mean_e) / sum(cnt), then M2 = sum(M2_e + cnt * (mean_e - mean)^2) —
-// the exact combination of equal-count partials, with sums instead of per-entry Chan merges (no
-// division per entry). Then the group's channels get A/B.
+// one block per (group g, image n). Every entry of a source holds `cnt` values (mean, M2). One fp64
+// pass over the group's entries (all granules, both concat sources) collects n = sum(cnt),
+// S1 = sum(cnt * mean_e) and S2 = sum(M2_e + cnt * mean_e^2); then mean = S1 / n and
+// M2 = S2 - n * mean^2 (fp64 keeps the cancellation far below fp32 resolution for GroupNorm inputs).
+// One block reduction of the three sums (was: two passes and three reductions).
+__device__ __forceinline__ void block_sum64x3(double& a, double& b, double& c, double* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b += __shfl_xor(b, o);
+    c += __shfl_xor(c, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[3 * w] = a;
+    sh[3 * w + 1] = b;
+    sh[3 * w + 2] = c;
+  }
+  __syncthreads();
+  a = sh[0];
+  b = sh[1];
+  c = sh[2];
+  for (int i = 1; i < GN_NT / 64; ++i) {
+    a += sh[3 * i];
+    b += sh[3 * i + 1];
+    c += sh[3 * i + 2];
+  }
+}
+
 __global__ __launch_bounds__(GN_NT) void gn_finalize2_kernel(GnFinalize2Params p) {
-  __shared__ double sh[GN_NT / 64];
+  __shared__ double sh[3 * (GN_NT / 64)];
   const int g = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
   const int C = p.s0.C + p.s1.C;
   const int Cg = C / GN_G;
   const int ng = Cg / 4;  // granules of the group
-  // granule k of the group -> (source, granule index); entries strided over the block
-  auto walk = [&](auto&& f) {
-    for (int k = 0; k < ng; ++k) {
-      const int c = g * Cg + 4 * k;
-      const bool first = c < p.s0.C;
-      const GnSrc& S = first ? p.s0 : p.s1;
-      const int gr = (first ? c : c - p.s0.C) >> 2;
-      const int QP = S.C >> 2;
-      const float* base = S.part + ((size_t)n * QP + gr) * S.E * 2;  // the granule's entries, contiguous
-      for (int e = tid; e < S.E; e += GN_NT) f(base + (size_t)e * 2, (double)S.cnt);
+  double sn = 0.0, sm = 0.0, sq = 0.0;
+  for (int k = 0; k < ng; ++k) {
+    const int c = g * Cg + 4 * k;
+    const bool first = c < p.s0.C;
+    const GnSrc& S = first ? p.s0 : p.s1;
+    const int gr = (first ? c : c - p.s0.C) >> 2;
+    const int QP = S.C >> 2;
+    const float* base = S.part + ((size_t)n * QP + gr) * S.E * 2;  // the granule's entries, contiguous
+    const double cnt = (double)S.cnt;
+    for (int e = tid; e < S.E; e += GN_NT) {
+      const float2 o = *reinterpret_cast<const float2*>(base + (size_t)e * 2);
+      const double m = (double)o.x;
+      sn += cnt;
+      sm += cnt * m;
+      sq += (double)o.y + cnt * m * m;
     }
-  };
-  double sn = 0.0, sm = 0.0;
-  walk([&](const float* o, double cnt) {
-    sn += cnt;
-    sm += cnt * (double)o[0];
-  });
-  const double ntot = block_sum64(sn, sh);
-  const double mean = block_sum64(sm, sh) / ntot;
-  double s2 = 0.0;
-  walk([&](const float* o, double cnt) {
-    const double d = (double)o[0] - mean;
-    s2 += (double)o[1] + cnt * d * d;
-  });
-  const double m2 = block_sum64(s2, sh);
+  }
+  block_sum64x3(sn, sm, sq, sh);
+  const double ntot = sn;
+  const double mean = sm / ntot;
+  const double m2 = sq - ntot * mean * mean;
   const float meanf = (float)mean;
   const float rstd = (float)(1.0 / sqrt(m2 / ntot + (double)p.eps));
   for (int c = g * Cg + tid; c < (g + 1) * Cg; c += GN_NT) {
