@@ -513,14 +513,10 @@ __global__ __launch_bounds__(NT, XF == XF_DOWN ? 2 : 4) void conv_kernel(ConvPar
 
 template <int BM, int BN, int WGM, int WGN, int TAPS, int XF, int MAXI, bool ONEIMG>
 static int launch_inst(const ConvParams& p, size_t lds, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_kernel<BM, BN, WGM, WGN, TAPS, XF, MAXI, ONEIMG>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
+  static bool attr_set[kMaxDevices] = {};
+  hipError_t e = set_lds_attr_once(
+      attr_set, reinterpret_cast<const void*>(&conv_kernel<BM, BN, WGM, WGN, TAPS, XF, MAXI, ONEIMG>), 160 * 1024);
+  if (e != hipSuccess) return (int)e;
   const int ptiles = (p.npix_tiles + 7) / 8 * 8;
   dim3 grid(ptiles * (p.cout_pad / BN), 1, p.ksplit);
   hipLaunchKernelGGL((conv_kernel<BM, BN, WGM, WGN, TAPS, XF, MAXI, ONEIMG>), grid, dim3(NT), lds, stream, p);

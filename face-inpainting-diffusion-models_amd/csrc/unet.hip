@@ -761,6 +761,10 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   // 3xf16: the split kernel has no avg-pool prologue or residual; a down-ResBlock's convs read
   // act+pool(x) / pool(x) materialised by act_pool at the output resolution instead (the same
   // fp32 arithmetic as conv.hip's XF_DOWN paths)
+  // o_pool2_ holds pool(in0) only for the conv that directly follows the act_pool that wrote it
+  // (conv2 of the same down-ResBlock); any other conv in between invalidates it
+  const float* pooled_prev = pooled_raw_;
+  pooled_raw_ = nullptr;
   if (split_ && cw.x3_ok) {
     const bool pool_in = xf == XF_DOWN && !in1;
     const bool pool_res = res && res_xf == XF_DOWN;
@@ -786,9 +790,8 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
         e = launch_act_pool(in0, c0, N, Hin, act, A, Bc, ws_ + o_pool_, raw_too ? ws_ + o_pool2_ : nullptr, s);
         pooled_raw_ = raw_too ? in0 : nullptr;
       }
-      if (!e && pool_res && res != pooled_raw_)
+      if (!e && pool_res && res != pooled_prev)
         e = launch_act_pool(res, cw.cout, N, resH, ACT_NONE, nullptr, nullptr, ws_ + o_pool2_, nullptr, s);
-      if (pool_res) pooled_raw_ = nullptr;
       prof_end(s, pe, "act_pool", 0.0, 4.0 * N * (double)Hin * Hin * (c0 + (pool_res ? cw.cout : 0)) * 1.25);
       IFD_REQUIRE(e == 0, "act_pool launch");
       p = q;
