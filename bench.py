@@ -139,9 +139,11 @@ def spawn_ranks(n):
 
 
 def train_main(args):
-    """`--workload train`: BASELINE configs[4]'s training step (code/train_inpainting.py:15-79), fp32 as the
-    reference trains (no bf16 / LoRA exists in the reference), B images per GPU at 256x256: t ~ randint,
-    training_losses with injection, backward, clip_grad_norm_(1.0), AdamW. Step = one optimizer step.
+    """`--workload train`: BASELINE configs[4]'s training step (code/train_inpainting.py:15-79), B images per GPU
+    at 256x256: t ~ randint, training_losses with injection, backward, clip_grad_norm_(1.0), AdamW. Step = one
+    optimizer step. --precision 3xf16 (default): forward and dgrad 3x3 convs on the fp32-accurate split
+    kernel (ifd/train.py UNetTrainer precision="3xf16"); fp32: every conv on fp32 MFMA, as the reference
+    trains (no bf16 / LoRA exists in the reference). At N=1 the other mode is timed beside it.
     Multi-GPU: per-rank steps (data parallelism would add an all-reduce of the 374 MB gradient; not part of
     the reference, which trains on one device)."""
     from ifd import parallel
@@ -154,38 +156,114 @@ def train_main(args):
     torch.cuda.set_device(dev)
     parallel.init(device=dev)
     B, H = args.batch, FULL.image_size
-    tr = UNetTrainer(FULL, device=dev)
-    tr.load_state_dict(make_state_dict(FULL, seed=1))
+    prec = "fp32" if args.precision == "fp32" else "3xf16"
     diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="quadratic")
     gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
     masked = gt * (1 - mask)
-    gen = torch.Generator(device=dev).manual_seed(1 + rank)
+    sd = make_state_dict(FULL, seed=1)
 
-    def step():
-        t = torch.randint(0, 1000, (B,), device=dev, generator=gen)
-        return tr.train_step(diff, gt, masked, mask, t)
-    for _ in range(args.warmup):
-        step()
+    def run(precision, steps, warmup):
+        tr = UNetTrainer(FULL, device=dev, precision=precision)
+        tr.load_state_dict(sd)
+        gen = torch.Generator(device=dev).manual_seed(1 + rank)
+
+        def step():
+            t = torch.randint(0, 1000, (B,), device=dev, generator=gen)
+            return tr.train_step(diff, gt, masked, mask, t)
+        for _ in range(warmup):
+            step()
+        parallel.barrier(dev)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = step()
+        torch.cuda.synchronize(dev)
+        parallel.barrier(dev)
+        el = parallel.max_over_ranks(time.perf_counter() - t0, dev)
+        lv = float(loss)
+        assert math.isfinite(lv)
+        trips = tr.guard_trips
+        del tr
+        torch.cuda.empty_cache()
+        return el, lv, trips
+
+    elapsed, lossv, trips = run(prec, args.steps, args.warmup)
+    value = B * ws * args.steps / elapsed
+    gf = gflop_per_image(FULL)
+    res = {"metric": f"training step images/sec ({prec} fwd+bwd+clip+AdamW, 256x256 9-ch UNet)", "value": round(value, 4),
+           "unit": "images/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None,
+           "dtype": "f32" if prec == "fp32" else "f32 (3xf16 split MFMA for the forward + dgrad 3x3 convs)",
+           "data": "synthetic (gt~U(-1,1), rectangle masks, seeded weights)",
+           "config": {"workload": "train_inpainting.py train_epoch step (BASELINE configs[4]; the reference trains "
+                                  "fp32 and has no bf16/LoRA)", "global_batch": B * ws, "batch_per_gpu": B,
+                      "parallelism": f"{ws} independent ranks"},
+           "loss": lossv, "guard_trips": trips,
+           "algorithmic_tflops": round(3 * gf * B * ws * args.steps / elapsed / 1e3, 2)}
+    if ws == 1 and args.fp32_exact_steps > 0 and prec != "fp32":
+        el2, _, _ = run("fp32", args.fp32_exact_steps, 1)
+        res["fp32_exact"] = {"value": round(B * args.fp32_exact_steps / el2, 4), "unit": "images/s",
+                             "ms_per_step": round(el2 / args.fp32_exact_steps * 1e3, 2),
+                             "steps": args.fp32_exact_steps}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def ddpm_main(args):
+    """`--workload ddpm`: BASELINE configs[2] (CelebA-HQ-shaped 256x256, B = 64 per GPU, DDPM-1000 linear,
+    code/tes_ddpm.py:402-468): step = one full 1000-eval inpainting_p_sample_loop + final blend over B
+    synthetic images; value = images/s. A full-step stress of the fused DDPM epilogue at B = 64 (the
+    workspace arena at this batch is reported); not the headline line."""
+    from ifd import parallel
+    from ifd.manifest import make_state_dict
+    from ifd.model import DiffusionInpaintingModel
+    from ifd.sampler import InpaintingSampler
+    from ifd.schedules import create_gaussian_diffusion
+    from ifd.topology import FULL, gflop_per_image
+    rank, ws, local = parallel.world()
+    dev = parallel.device_for(local)
+    torch.cuda.set_device(dev)
+    parallel.init(device=dev)
+    B, H = args.batch, FULL.image_size
+    model = DiffusionInpaintingModel(FULL, device=dev, precision=args.precision)
+    model.load_state_dict(make_state_dict(FULL, seed=1))
+    diffusion = create_gaussian_diffusion(steps=args.ddpm_steps, learn_sigma=True, noise_schedule="linear")
+    sampler = InpaintingSampler(model, diffusion, device=dev)
+    gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
+
+    def one_pass(i):
+        torch.manual_seed(42 + 1000 * rank + i)
+        with torch.no_grad():
+            y = sampler.inpainting_p_sample_loop(sampler.model_fn, (B, 3, H, H), gt, mask, True, dev, False)
+            return parallel.gather_images(sampler.final_blend(y, gt, mask), B * ws)
+    for i in range(args.warmup):
+        one_pass(i)
     parallel.barrier(dev)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
+    for i in range(args.steps):
+        y = one_pass(args.warmup + i)
     torch.cuda.synchronize(dev)
     parallel.barrier(dev)
     elapsed = parallel.max_over_ranks(time.perf_counter() - t0, dev)
-    lossv = float(loss)
-    assert math.isfinite(lossv)
-    value = B * ws * args.steps / elapsed
-    gf = gflop_per_image(FULL)
-    res = {"metric": "training step images/sec (fp32 fwd+bwd+clip+AdamW, 256x256 9-ch UNet)", "value": round(value, 4),
-           "unit": "images/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "f32", "data": "synthetic (gt~U(-1,1), rectangle masks, seeded weights)",
-           "config": {"workload": "train_inpainting.py train_epoch step (BASELINE configs[4], fp32: the reference has no "
-                                  "bf16/LoRA)", "global_batch": B * ws, "batch_per_gpu": B,
-                      "parallelism": f"{ws} independent ranks"},
-           "loss": lossv, "algorithmic_tflops": round(3 * gf * B * ws * args.steps / elapsed / 1e3, 2)}
+    assert torch.isfinite(y).all()
+    n_evals = diffusion.num_timesteps
+    res = {"metric": "256x256 DDPM-1000 inpainted images/sec (BASELINE configs[2], full-step stress)",
+           "value": round(B * ws * args.steps / elapsed, 4), "unit": "images/s", "n_gpus": ws, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+           "unet_ms_per_eval": round(elapsed / args.steps / n_evals * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else
+           f"f32 ({args.precision} conv arithmetic)", "data": "synthetic",
+           "config": {"workload": f"256x256 9-ch UNet inpainting, DDPM-{n_evals} linear (configs[2])",
+                      "global_batch": B * ws, "batch_per_gpu": B, "unet_evals_per_image": n_evals},
+           "algorithmic_tflops": round(gflop_per_image(FULL) * B * ws * n_evals * args.steps / elapsed / 1e3, 2),
+           "torch_max_memory_allocated_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)}
+    import ctypes
+    from ifd import _lib
+    wb, wsb = ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.lib().ifd_memory(model.handle(dev).h, ctypes.byref(wb), ctypes.byref(wsb)))
+    res["library_memory_gb"] = {"weights": round(wb.value / 1e9, 3), "workspace": round(wsb.value / 1e9, 3)}
     if rank == 0:
         print(json.dumps(res), flush=True)
 
@@ -207,8 +285,9 @@ def main():
     ap.add_argument("--f16-steps", type=int, default=1,
                     help="N=1 only: also time this many steps in the reduced-precision f16 mode, reported separately "
                          "(the reference's .half() experiment, code/test_quant.py:390-409; 0 = skip)")
-    ap.add_argument("--workload", choices=["sample", "train"], default="sample",
-                    help="sample: the headline DDIM-100 sampler (default); train: the training step (configs[4])")
+    ap.add_argument("--ddpm-steps", type=int, default=1000, help="--workload ddpm: diffusion steps T (linear)")
+    ap.add_argument("--workload", choices=["sample", "train", "ddpm"], default="sample",
+                    help="sample: the headline DDIM-100 sampler (default); train: the training step (configs[4]); ddpm: DDPM-1000 at B=64 (configs[2])")
     ap.add_argument("--noise", choices=["device", "parity"], default="device",
                     help="device: per-rank GPU RNG (throughput); parity: full-batch host draws in reference order, "
                          "sliced per rank (GPU-count-independent results)")
@@ -217,6 +296,8 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     if args.workload == "train":
         return train_main(args)
+    if args.workload == "ddpm":
+        return ddpm_main(args)
 
     from ifd import parallel
     from ifd.manifest import make_state_dict

@@ -900,6 +900,46 @@ __global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float
   p[i] = pi;
 }
 
+
+// 3xf16 split packing of a 3x3 conv weight on the device (unet.hip pack_conv_x3's layout and
+// arithmetic): one thread per (ct, chunk, tap, h, col, j) writes both parts.
+__global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int cin, int cin_pad16, int cout_pad,
+                                    int transpose, _Float16* __restrict__ dst, unsigned* guard) {
+#pragma clang fp contract(off)
+  const int nch = cin_pad16 / 16;
+  const int64_t tot = (int64_t)(cout_pad / 64) * nch * 9 * 2 * 64 * 8;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int j = (int)(i & 7);
+  int64_t r = i >> 3;
+  const int col = (int)(r & 63);
+  r >>= 6;
+  const int hh = (int)(r & 1);
+  r >>= 1;
+  const int tap = (int)(r % 9);
+  r /= 9;
+  const int chk = (int)(r % nch);
+  const int ct = (int)(r / nch);
+  const int o = ct * 64 + col, c = chk * 16 + hh * 8 + j;  // packed (out, in) channel
+  float v = 0.f;
+  if (transpose == 0) {
+    if (o < cout && c < cin) v = w[((size_t)o * cin + c) * 9 + tap];
+  } else {
+    if (o < cin && c < cout) v = w[((size_t)c * cin + o) * 9 + (8 - tap)];
+  }
+  const _Float16 hi = (_Float16)v;
+  const float s = (float)hi * 2048.0f;
+  if (!(fabsf(s) <= 65504.0f)) atomicOr(guard, 2u);
+  const _Float16 lo = (_Float16)((v - (float)hi) * 2048.0f);
+  const size_t base = ((((size_t)ct * nch + chk) * 9 + tap) * 2) * 2;  // part 0
+  dst[((base + hh) * 64 + col) * 8 + j] = (_Float16)s;
+  dst[((base + 2 + hh) * 64 + col) * 8 + j] = lo;
+}
+
+__global__ void scale_kernel(float* __restrict__ x, int64_t n, float s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = x[i] * s;
+}
 }  // namespace
 }  // namespace ifd
 
@@ -966,6 +1006,70 @@ int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, 
   if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, (hipStream_t)stream);
   if (e) set_error(std::string("ifd_tr_conv: ") + hipGetErrorString((hipError_t)e));
   return e;
+}
+
+int ifd_tr_pack_conv_x3(const float* w, int cout, int cin, int taps, int cin_pad16, int cout_pad, int transpose,
+                        void* wx3, unsigned* guard, void* stream) {
+  if (!w || !wx3 || !guard || taps != 9 || cin_pad16 % 16 || cout_pad % 64) {
+    set_error("ifd_tr_pack_conv_x3: bad arguments");
+    return 2;
+  }
+  const int64_t tot = (int64_t)(cout_pad / 64) * (cin_pad16 / 16) * 9 * 2 * 64 * 8;
+  hipLaunchKernelGGL(pack_conv_x3_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, w, cout, cin, cin_pad16,
+                     cout_pad, transpose, (_Float16*)wx3, guard);
+  return TR_LAST();
+}
+
+static void conv_x3_params(ConvParams& p, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                           const void* wx3, const float* bias, int cin_pad, int cout, const float* res, float* out) {
+  conv_params(p, x0, c0, x1, c1, N, H, (const float*)wx3, bias, cin_pad, cout, cout, 64, 9, res, out);
+  p.opt_bm128 = 0;
+  p.x3_nprod = 3;
+  conv_geometry(p, H, H, N, 64, cin_pad / 16, true);
+}
+
+int64_t ifd_tr_conv_x3_part_floats(int N, int H, int cin_pad, int cout) {
+  ConvParams p;
+  conv_x3_params(p, nullptr, cin_pad, nullptr, 0, N, H, nullptr, nullptr, cin_pad, cout, nullptr, nullptr);
+  return p.ksplit > 1 ? (int64_t)p.ksplit * N * H * H * cout : 0;
+}
+
+int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3, const float* bias,
+                   int cin_pad, int cout, const float* res, float* out, float* part, int64_t part_floats,
+                   unsigned* guard, void* stream) {
+  if ((H & (H - 1)) || c0 + c1 != cin_pad || !x0 || !out || !wx3 || !bias || !guard) {
+    set_error("ifd_tr_conv_x3: unsupported arguments");
+    return 2;
+  }
+  ConvParams p;
+  conv_x3_params(p, x0, c0, c1 ? x1 : nullptr, c1, N, H, wx3, bias, cin_pad, cout, res, out);
+  p.guard = guard;
+  const int nct = cout / 64;  // the non-SKIP split kernel decodes channel tiles by shifts
+  if (cout % 64 || (nct & (nct - 1)) || !conv_x3_eligible(p, 9, XF_NONE, 64)) {
+    set_error("ifd_tr_conv_x3: shape not eligible for the split kernel (use ifd_tr_conv)");
+    return 3;
+  }
+  if (p.ksplit > 1) {
+    if (!part || (int64_t)p.ksplit * N * H * H * cout > part_floats) {
+      set_error("ifd_tr_conv_x3: split-K workspace too small (ifd_tr_conv_x3_part_floats)");
+      return 2;
+    }
+    p.part = part;
+  }
+  int e = launch_conv_x3(p, XF_NONE, (hipStream_t)stream);
+  if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, (hipStream_t)stream);
+  if (e) set_error(std::string("ifd_tr_conv_x3: ") + hipGetErrorString((hipError_t)e));
+  return e;
+}
+
+int ifd_tr_scale(float* x, int64_t n, float s, void* stream) {
+  if (!x || n < 0) {
+    set_error("ifd_tr_scale: bad arguments");
+    return 2;
+  }
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(scale_kernel, dim3(grid1(n)), dim3(TB), 0, (hipStream_t)stream, x, n, s);
+  return TR_LAST();
 }
 
 // split-K count of wgrad9_kernel: blocks (tiles x splits) >= ~2 per CU, >= 8 chunks per split

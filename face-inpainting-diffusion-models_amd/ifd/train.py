@@ -34,6 +34,10 @@ vp, i32, i64, f32 = _c.c_void_p, _c.c_int, _c.c_int64, _c.c_float
 TRAIN_EXPORTS = {
     "ifd_tr_pack_conv": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
     "ifd_tr_conv_part_floats": (i64, [i32, i32, i32, i32, i32, i32, i32]),
+    "ifd_tr_pack_conv_x3": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "ifd_tr_conv_x3_part_floats": (i64, [i32, i32, i32, i32]),
+    "ifd_tr_conv_x3": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, vp]),
+    "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
     "ifd_tr_conv_wgrad": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp]),
@@ -88,10 +92,25 @@ def _pad(v, m):
 
 
 class UNetTrainer:
-    """fp32 training of the 9-channel UNet (code/unet.py:14-200) with the reference's loss, clip and AdamW."""
+    """fp32 training of the 9-channel UNet (code/unet.py:14-200) with the reference's loss, clip and AdamW.
+
+    precision="3xf16": the 3x3 convs of the forward (and, with x3_dgrad, the dgrad convs of the backward)
+    run on the sampler's fp32-accurate split kernel (conv_x3.hip: each fp32 operand = f16 hi + f16 lo,
+    three f16 MFMA products per MAC, fp32 accumulation). The backward then carries a loss scale of
+    2^x3_loss_scale_log2 (the eps-MSE gradient is ~1e-7 per element: below f16's normal range unscaled);
+    every backward op is linear in the upstream gradient and the scale is a power of two, so removing it
+    from the parameter gradients before clip + AdamW is exact. A split operand outside f16's range sets
+    the range guard; the step is then recomputed in fp32 (same noise) with a warning. wgrad, GroupNorm,
+    attention, embeddings and the optimizer stay fp32."""
 
     def __init__(self, cfg: UNetConfig = FULL, device="cuda", lr=5e-5, weight_decay=0.01, betas=(0.9, 0.999),
-                 eps=1e-8, max_norm=1.0):
+                 eps=1e-8, max_norm=1.0, precision="fp32", x3_dgrad=True, x3_loss_scale_log2=20):
+        if precision not in ("fp32", "3xf16"):
+            raise ValueError(f"precision must be 'fp32' or '3xf16', got {precision!r}")
+        self.precision = precision
+        self.x3_dgrad = bool(x3_dgrad)
+        self.x3_loss_scale_log2 = int(x3_loss_scale_log2)
+        self.guard_trips = 0
         self.cfg = cfg
         self.dev = torch.device(device)
         self.lr, self.wd, self.betas, self.eps, self.max_norm = lr, weight_decay, betas, eps, max_norm
@@ -115,6 +134,9 @@ class UNetTrainer:
         self.plan = layer_plan(cfg)
         self.emb_dim = 4 * cfg.model_channels
         self.s = None  # stream pointer (set per call)
+        self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
+        self._grad_clean = False
+        self._pack_cache = {}
 
     # ------------------------------------------------------------------ parameters
     def p(self, name):
@@ -163,9 +185,45 @@ class UNetTrainer:
             self._pack_cache[key] = buf
         return buf, pout, pin, taps, bn, cin_pad, cout_pad
 
+    def _x3_active(self, transpose):
+        return self.precision == "3xf16" and (not transpose or self.x3_dgrad)
+
+    def _conv_x3(self, x, cin_x, N, H, name, bias_name, res, x1, c1, transpose):
+        """The conv on the 3xf16 split kernel, or None when its shape is not eligible (fp32 kernel then)."""
+        w = self.p(name)
+        if w.dim() != 4 or w.shape[2] * w.shape[3] != 9:
+            return None
+        cout, cin = w.shape[0], w.shape[1]
+        pout, pin = (cout, cin) if not transpose else (cin, cout)
+        nct = pout // 64
+        if pout % 64 or nct & (nct - 1) or cin_x + c1 != _pad(pin, 16) or cin_x % 16 or c1 % 16:
+            return None
+        cin_pad = cin_x + c1
+        key = (name, int(transpose), "x3")
+        wx3 = self._pack_cache.get(key)
+        if wx3 is None:
+            wx3 = self._empty(pout * cin_pad * 9)
+            chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, 9, cin_pad, pout, int(transpose), P(wx3), P(self._guard),
+                                          self.s))
+            self._pack_cache[key] = wx3
+        b = self.p(bias_name) if bias_name else self._zero_bias
+        out = self._empty(N, H, H, pout)
+        pf = lib().ifd_tr_conv_x3_part_floats(N, H, cin_pad, pout)
+        part = self._empty(max(pf, 1))
+        rc = lib().ifd_tr_conv_x3(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, pout, P(res), P(out), P(part), pf,
+                                  P(self._guard), self.s)
+        if rc == 3:
+            return None
+        chk(rc)
+        return out
+
     def conv(self, x, cin_x, N, H, name, bias_name=None, res=None, x1=None, c1=0, transpose=False):
         """NHWC conv of concat(x[cin_x], x1[c1]) with weight `name` (forward or, transposed, dgrad).
         Output channels are padded to a multiple of 4 (zero weight rows): the 6-channel head writes 8."""
+        if self._x3_active(transpose):
+            out = self._conv_x3(x, cin_x, N, H, name, bias_name, res, x1, c1, transpose)
+            if out is not None:
+                return out
         buf, pout, pin, taps, bn, cin_pad, cout_pad = self._packed(name, int(transpose))
         if cin_x + c1 != cin_pad:
             raise ValueError(f"{name}: input channels {cin_x}+{c1} != packed {cin_pad}")
@@ -340,8 +398,20 @@ class UNetTrainer:
         saved[p] = dict(x=x, n=n, st=st, qkv=qkv, a=a, scale=scale)
         return out
 
-    def backward(self, dout6):
-        """Gradients of every parameter (+= into the flat grad buffer) from d loss / d out6 (NHWC)."""
+    def backward(self, dout6, grad_scale=None):
+        """Gradients of every parameter (+= into the flat grad buffer) from d loss / d out6 (NHWC).
+        grad_scale: the factor dout6 carries (default: the 3xf16 loss scale when dout6 is the loss's own
+        gradient); the accumulated gradients are brought to it first and divided by it after (exact)."""
+        if grad_scale is None:
+            grad_scale = getattr(self, "_gscale", 1.0) if dout6 is getattr(self, "_dout6", None) else 1.0
+        if grad_scale != 1.0 and not self._grad_clean:
+            chk(lib().ifd_tr_scale(P(self.grad), self.numel, grad_scale, _lib.stream_ptr(self.dev)))
+        self._backward(dout6)
+        if grad_scale != 1.0:
+            chk(lib().ifd_tr_scale(P(self.grad), self.numel, 1.0 / grad_scale, self.s))
+        self._grad_clean = False
+
+    def _backward(self, dout6):
         tape = self._tape
         N, H = tape["N"], tape["H"]
         saved = tape["saved"]
@@ -476,17 +546,27 @@ class UNetTrainer:
         chk(lib().ifd_tr_q_sample_inject(P(x0c), P(nc_), P(cached.contiguous()), P(mc), P(tt), P(sa), P(s1m), N,
                                          H * W, int(inject), P(xt), self.s))
         mi = masked.to(self.dev, torch.float32).contiguous() if masked is not None else self._zeros(N, 3, H, W)
+        self._keep = (xt, mi, mc, nc_, x0c, tt)
+        return self._forward_loss(xt, tt, mi, mc, nc_)
+
+    def _forward_loss(self, xt, tt, mi, mc, nc_):
+        """UNet forward + masked eps-MSE; keeps d loss / d out6 (times the 3xf16 loss scale) for backward."""
+        N, _, H, W = xt.shape
         out6 = self.forward(xt, tt, mi, mc)  # [N, H, W, 8]: channels 0-5 the model output
         cs = out6.shape[-1]
         self._dout6 = self._empty(N, H, W, cs)
         work = self._empty(N * 6)
         chk(lib().ifd_tr_masked_mse(P(out6), cs, P(nc_), P(mc), N, H * W, P(self.loss), P(self._dout6), P(work),
                                     self.s))
-        self._keep = (xt, mi, mc, nc_, x0c, tt)
+        self._gscale = 1.0
+        if self._x3_active(True):
+            self._gscale = float(2.0 ** self.x3_loss_scale_log2)
+            chk(lib().ifd_tr_scale(P(self._dout6), self._dout6.numel(), self._gscale, self.s))
         return self.loss
 
     def zero_grad(self):
         self.grad.zero_()
+        self._grad_clean = True
 
     def optimizer_step(self):
         """clip_grad_norm_(max_norm) + AdamW (code/train_inpainting.py:64-66); norm on device, no sync."""
@@ -499,11 +579,27 @@ class UNetTrainer:
 
     def train_step(self, diffusion, images, masked_images, masks, t, noise=None, noise_device=None):
         """One iteration of train_epoch (code/train_inpainting.py:27-66): zero_grad, training_losses,
-        backward, clip_grad_norm_(1.0), AdamW.step(). Returns the loss as a device scalar."""
+        backward, clip_grad_norm_(1.0), AdamW.step(). Returns the loss as a device scalar.
+        3xf16: one host read of the range guard per step; a trip recomputes the step in fp32."""
         self.zero_grad()
+        if self.precision == "3xf16":
+            self._guard.zero_()
         loss = self.training_loss(diffusion, images, t, {"masked_image": masked_images, "mask": masks}, noise=noise,
                                   noise_device=noise_device)
         self.backward(self._dout6)
+        if self.precision == "3xf16" and int(self._guard[0].item()):
+            import warnings
+            warnings.warn("3xf16 range guard tripped (an operand or weight outside the f16 split's range): "
+                          "step recomputed in fp32")
+            self.guard_trips += 1
+            self.precision = "fp32"
+            try:
+                self.zero_grad()
+                xt, mi, mc, nc_, _x0, tt = self._keep
+                loss = self._forward_loss(xt, tt, mi, mc, nc_)
+                self.backward(self._dout6)
+            finally:
+                self.precision = "3xf16"
         self.optimizer_step()
         return loss
 

@@ -33,6 +33,21 @@ int64_t ifd_tr_conv_part_floats(int N, int H, int cin_pad, int cout, int cout_pa
 int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* wpack, const float* bias,
                 int cin_pad, int cout, int cout_pad, int bn, int taps, const float* res, float* out, float* part,
                 int64_t part_floats, void* stream);
+/* 3xf16 training convs (the sampler's split kernel, conv_x3.hip, on a materialised input: no prologue).
+ * ifd_tr_pack_conv_x3: W[cout][cin][9] (transpose=1: the dgrad conv, taps flipped) -> the split packing
+ * [cout_pad/64][cin_pad16/16][9][part][h][64][8] f16 (wx3: cout_pad * cin_pad16 * 9 floats); sets bit 2 of
+ * *guard when a weight is outside the split's range (|w| >= 32).
+ * ifd_tr_conv_x3: the same contract as ifd_tr_conv for 3x3 convs with cout % 64 == 0, cin % 16 == 0 and
+ * maps of >= 16x16 (8x8: N % 4 == 0); returns 3 (nothing launched) for any other shape, so the caller runs
+ * ifd_tr_conv. Operands with |a| >= 65504 set bit 1 of *guard (the step must then be re-run in fp32). */
+int ifd_tr_pack_conv_x3(const float* w, int cout, int cin, int taps, int cin_pad16, int cout_pad, int transpose,
+                        void* wx3, unsigned* guard, void* stream);
+int64_t ifd_tr_conv_x3_part_floats(int N, int H, int cin_pad, int cout);
+int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3, const float* bias,
+                   int cin_pad, int cout, const float* res, float* out, float* part, int64_t part_floats,
+                   unsigned* guard, void* stream);
+/* x[i] *= s (the loss scale of the 3xf16 backward and its removal from the gradients). */
+int ifd_tr_scale(float* x, int64_t n, float s, void* stream);
 /* dw[cout][c0+c1][taps] += sum_pixels dy (x) shifted concat(x0, x1); db[cout] += column sums of dy. */
 int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* splits);
 int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,

@@ -37,12 +37,15 @@ def golden_train():
     return meta, dict(np.load(os.path.join(GOLDEN, "train_steps.npz")))
 
 
-def test_train_steps_match_reference(golden_train, record):
+@pytest.mark.parametrize("precision", ["fp32", "3xf16"])
+def test_train_steps_match_reference(golden_train, record, precision):
+    """Both modes at the same tolerances. 3xf16: the reduced config's 64-channel 3x3 convs (forward and
+    dgrad) run on the split kernel, its 32-channel ones stay fp32 (cout % 64)."""
     from ifd.schedules import create_gaussian_diffusion
     from ifd.train import UNetTrainer
     meta, z = golden_train
     tr = UNetTrainer(REDUCED, device=DEV, lr=meta["lr"], weight_decay=meta["weight_decay"], betas=tuple(meta["betas"]),
-                     eps=meta["eps"], max_norm=meta["max_norm"])
+                     eps=meta["eps"], max_norm=meta["max_norm"], precision=precision)
     tr.load_state_dict(make_state_dict(REDUCED, seed=1))
     diff = create_gaussian_diffusion(steps=meta["T"], learn_sigma=True, noise_schedule=meta["schedule"])
     lr = meta["lr"]
@@ -89,7 +92,8 @@ def test_train_steps_match_reference(golden_train, record):
         assert rel_loss <= 1e-5 and rel_gn <= 1e-4, worst[step]
         assert g_rel <= 1e-3 and n_rel <= 1e-3, worst[step]
         assert d_err <= 1e-3, worst[step]
-    record("train_steps_reduced/fp32", **{f"step{k}": v for k, v in worst.items()})
+    assert tr.guard_trips == 0
+    record(f"train_steps_reduced/{precision}", **{f"step{k}": v for k, v in worst.items()})
 
 
 def test_train_step_deterministic():
@@ -109,3 +113,71 @@ def test_train_step_deterministic():
         torch.cuda.synchronize()
         outs.append(tr.flat.clone())
     assert torch.equal(outs[0], outs[1])
+
+
+def _full_step(precision, B=4, scale_conv_in=1.0, **kw):
+    from bench import synth_inputs
+    from ifd.schedules import create_gaussian_diffusion
+    from ifd.topology import FULL
+    from ifd.train import UNetTrainer
+    diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="quadratic")
+    gt, mask = synth_inputs(B, FULL.image_size, seed=5, device=DEV)
+    tr = UNetTrainer(FULL, device=DEV, precision=precision, **kw)
+    sd = make_state_dict(FULL, seed=1)
+    if scale_conv_in != 1.0:
+        sd = dict(sd)
+        for k in sd:
+            if k.endswith("input_blocks.0.0.weight"):
+                sd[k] = sd[k] * scale_conv_in
+    tr.load_state_dict(sd)
+    torch.manual_seed(11)
+    t = torch.randint(0, 1000, (B,), device=DEV)
+    noise = torch.randn(B, 3, FULL.image_size, FULL.image_size, device=DEV)
+    torch.manual_seed(12)
+    loss = float(tr.train_step(diff, gt, gt * (1 - mask), mask, t, noise=noise))
+    torch.cuda.synchronize()
+    return tr, loss
+
+
+def test_train_x3_full_matches_fp32(record):
+    """Full 256^2 config, B = 4: one 3xf16 step (forward + dgrad on the split kernel, loss scale 2^20)
+    against the fp32 step from the same state, noise and GT-noise cache draw. Gates: loss relative 1e-5,
+    global grad norm relative 1e-5, every parameter gradient ||g - g_fp32|| <= 1e-4 ||g_fp32|| (the fp32
+    step vs the reference's own: <= 6e-6 on the reduced config), and no range-guard trip."""
+    tr32, l32 = _full_step("fp32")
+    g32 = tr32.grad.clone()
+    n32 = float(tr32.norm_coef[0])
+    offs = tr32.offsets
+    del tr32
+    tr3, l3 = _full_step("3xf16")
+    assert tr3.guard_trips == 0
+    rel_loss = abs(l3 - l32) / abs(l32)
+    rel_gn = abs(float(tr3.norm_coef[0]) - n32) / n32
+    worst, wname = 0.0, None
+    for k, (o, shape) in offs.items():
+        n = int(np.prod(shape))
+        a, b = tr3.grad[o:o + n].double(), g32[o:o + n].double()
+        bn = float(b.norm())
+        if bn == 0.0:
+            continue
+        r = float((a - b).norm()) / bn
+        if r > worst:
+            worst, wname = r, k
+    record("train_x3_full_vs_fp32", loss=l3, loss_fp32=l32, rel_loss=rel_loss, rel_grad_norm=rel_gn,
+           max_tensor_grad_rel=worst, worst_tensor=wname)
+    assert rel_loss <= 1e-5 and rel_gn <= 1e-5, (rel_loss, rel_gn)
+    assert worst <= 1e-4, (worst, wname)
+
+
+def test_train_x3_range_guard():
+    """A conv_in weight scaled x1e5 puts the forward operands of the next conv beyond f16's range (and
+    the weights beyond the split's |w| < 32): the guard trips and the step is recomputed in fp32,
+    bit-identical to the fp32 step."""
+    tr32, l32 = _full_step("fp32", B=4, scale_conv_in=1e5)
+    p32 = tr32.flat.clone()
+    del tr32
+    with pytest.warns(UserWarning, match="range guard"):
+        tr3, l3 = _full_step("3xf16", B=4, scale_conv_in=1e5)
+    assert tr3.guard_trips == 1
+    assert l3 == l32
+    assert torch.equal(tr3.flat, p32)
