@@ -628,6 +628,10 @@ class BlockTrainer(UNetTrainer):
         self.grad = torch.zeros(n, device=self.dev)
         self._zero_bias = torch.zeros(4096, device=self.dev)
         self._pack_cache = {}
+        self.precision, self.x3_dgrad, self.x3_loss_scale_log2, self.guard_trips = "fp32", False, 0, 0
+        self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
+        self._grad_clean = False
+        self._pack_cache = {}
         self.s = None
 
     def load_state_dict(self, sd):
