@@ -597,8 +597,15 @@ __global__ void splitk_reduce_kernel(ConvParams p) {
   if (i >= tot) return;
   const int co = (int)(i % p.cout);
   const size_t pix = i / p.cout;
-  float acc = p.part[i];
-  for (int z = 1; z < p.ksplit; ++z) acc += p.part[(size_t)z * tot + i];
+  float sl[8];
+#pragma unroll
+  for (int z = 0; z < 8; ++z)
+    if (z < p.ksplit) sl[z] = p.part[(size_t)z * tot + i];
+  float acc = sl[0];
+#pragma unroll
+  for (int z = 1; z < 8; ++z)
+    if (z < p.ksplit) acc += sl[z];
+  for (int z = 8; z < p.ksplit; ++z) acc += p.part[(size_t)z * tot + i];
   float v = acc + p.bias[co];
   if (p.res) {
     const int x = (int)(pix % p.W), y = (int)((pix / p.W) % p.H), n = (int)(pix / ((size_t)p.W * p.H));
@@ -630,6 +637,7 @@ __global__ void splitk_reduce_kernel(ConvParams p) {
 // epilogues (gstat[n][cout/4][e] = (mean, M2), e = slice, cnt = 4 * SKG_SL values). 8 quads x
 // 32 pixel lanes per block: enough blocks even for the 8x8 layers (one slice per image).
 constexpr int SKG_SL = 64;
+constexpr int SKG_MAXS = 8;  // split-K counts conv_geometry produces (S <= 8)
 constexpr int SKG_Q = 8, SKG_PL = 256 / SKG_Q;
 __global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
   __shared__ float red[SKG_PL][SKG_Q][3];
@@ -649,8 +657,17 @@ __global__ __launch_bounds__(256) void splitk_gstat_kernel(ConvParams p) {
     for (int i = pl; i < slice; i += SKG_PL) {
       const int px = e * slice + i;
       const size_t idx = ((size_t)n * HW + px) * p.cout + 4 * qq;
-      f32x4 acc = gld4(p.part + idx);
-      for (int z = 1; z < p.ksplit; ++z) acc += gld4(p.part + (size_t)z * tot + idx);
+      // all slabs' loads in flight together (a runtime-bounded loop issued them one latency apart),
+      // summed in slab order as before
+      f32x4 sl[SKG_MAXS];
+#pragma unroll
+      for (int z = 0; z < SKG_MAXS; ++z)
+        if (z < p.ksplit) sl[z] = gld4(p.part + (size_t)z * tot + idx);
+      f32x4 acc = sl[0];
+#pragma unroll
+      for (int z = 1; z < SKG_MAXS; ++z)
+        if (z < p.ksplit) acc += sl[z];
+      for (int z = SKG_MAXS; z < p.ksplit; ++z) acc += gld4(p.part + (size_t)z * tot + idx);
       f32x4 v = acc + b;
       if (p.res) {
         const int x = px % p.W, y = px / p.W;

@@ -309,6 +309,193 @@ __global__ __launch_bounds__(256) void wgrad9_kernel(WgArgs a) {
     }
 }
 
+// 3xf16 weight gradient (training precision "3xf16"), all taps of a 64 co x 64 ci tile per block:
+//   dW[co][ci][tap] = sum_p dY[p][co] X[p + offset(tap)][ci]
+// with both operands split on the fly (hi = f16(v), lo = f16(v - hi), conv_x3.hip's split) and three
+// f16 products per MAC (dY_hi X_hi + dY_hi X_lo + dY_lo X_hi) into fp32 accumulators
+// (v_mfma_f32_32x32x16_f16, K = 16 output pixels). Per chunk of 64 output pixels (2 rows of 32, or
+// 64 / W whole rows) the block stages, pixel-major as they sit in HBM (16-B loads, no transpose):
+//   D [part][64 px][64 co]      X [part][halo px, row-major (R + 2) x (Wc + 2) <= 136][64 ci]   f16
+// and the MFMA operands, which want 8 consecutive pixels of one channel per lane, come from
+// ds_read_b64_tr_b16 (4 pixel rows x 16 channels per 16-lane group, delivered column-major): a tap's
+// shift only changes which halo rows a lane addresses. 16-B chunks of a row are XOR-swizzled by
+// bit 1 of the row, so the 4 rows x 64 B a 32-lane half reads cover all 64 banks once. Double-
+// buffered; wave w owns the 32 x 32 quadrant (co 32 (w & 1), ci 32 (w >> 1)) of all 9 taps (144
+// accumulator registers). dY carries the backward's loss scale; |v| >= 65504 sets the range guard.
+// (A first version staged both operands transposed through dword loads and read the shifted X rows
+// unaligned: it ran no faster than the fp32 wgrad9_kernel; the loads and the unaligned reads each
+// cost more than the MFMAs.)
+#ifndef WX_ABL
+#define WX_ABL 0  // development timing ablations: 2 no global loads after the first chunk
+#endif
+constexpr int WX_PX = 64;                 // output pixels per chunk
+constexpr int WX_HMAX = 136;              // halo pixels: 4 x 34, 6 x 18, 10 x 10
+constexpr int WX_D = 2 * WX_PX * 64;      // f16 per stage: dY, both parts
+constexpr int WX_X = 2 * WX_HMAX * 64;    // X halo, both parts
+constexpr int WX_DI = WX_PX * 16 / 256;   // dY 16-B items per thread (4)
+constexpr int WX_XI = (WX_HMAX * 16 + 255) / 256;  // X halo items per thread (9)
+typedef _Float16 wx_h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 wx_h4 __attribute__((ext_vector_type(4)));
+typedef unsigned wx_u2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) wx_u2 wx_lds_u2;
+
+// element offset of channel c (multiple of 4) of row r: 16-B chunk (c / 8) XOR 4 (bit 1 of r)
+__device__ __forceinline__ int wx_off(int r, int c) { return r * 64 + ((((c >> 3) ^ ((r & 2) << 1))) << 3) + (c & 7); }
+
+typedef __fp16 wx_hv4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+__device__ __forceinline__ wx_h4 wx_tr(const _Float16* L, int off) {
+  return __builtin_bit_cast(wx_h4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) wx_hv4*)(L + off)));
+}
+
+__global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
+  const int cin = a.c0;
+  const int nci = (cin + 63) / 64;
+  const int cit = blockIdx.x % nci, cot = blockIdx.x / nci;
+  const int co0 = cot * 64, ci0 = cit * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5;
+  const int wr = 32 * (wave & 1), wc = 32 * (wave >> 1);
+  const int Wc = a.W < 32 ? a.W : 32, R = WX_PX / Wc;
+  const int HWc = Wc + 2, HP = (R + 2) * HWc;
+  const int lwc = __builtin_ctz(Wc);
+  const int segs = a.W / Wc, rows_per_img = a.H / R;
+  const int64_t nch = (int64_t)a.N * rows_per_img * segs;
+  const int64_t c_beg = (int64_t)blockIdx.y * a.chunks_per_split;
+  const int64_t c_end = c_beg + a.chunks_per_split < nch ? c_beg + a.chunks_per_split : nch;
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float gmax = 0.f;
+  if (c_beg < c_end) {
+    // staging items: (pixel i >> 4, channel quad i & 15), i = tid + 256 k; quad fixed per thread
+    const int cq = tid & 15;
+    const bool co_ok = co0 + 4 * cq + 3 < a.cout, ci_ok = ci0 + 4 * cq + 3 < cin;
+    f32x4 dv[WX_DI], xv[WX_XI];
+    int xhy[WX_XI], xhx[WX_XI];
+#pragma unroll
+    for (int k = 0; k < WX_XI; ++k) {
+      const int hp = (tid + 256 * k) >> 4;
+      xhy[k] = hp < HP ? hp / HWc - 1 : -1000000;  // halo row / column relative to the chunk origin
+      xhx[k] = hp % HWc - 1;
+    }
+    auto chunk_origin = [&](int64_t c, int& n, int& y0, int& x0) {
+      const int64_t per_img = (int64_t)rows_per_img * segs;
+      n = (int)(c / per_img);
+      const int rem = (int)(c - (int64_t)n * per_img);
+      y0 = (rem / segs) * R;
+      x0 = (rem % segs) * Wc;
+    };
+    auto load = [&](int64_t c) {
+      if (WX_ABL == 2 && c != c_beg) return;
+      int n, y0, x0;
+      chunk_origin(c, n, y0, x0);
+      const int64_t img = (int64_t)n * a.H;
+#pragma unroll
+      for (int k = 0; k < WX_DI; ++k) {
+        const int m = (tid + 256 * k) >> 4;
+        const int64_t pix = (img + y0 + (m >> lwc)) * a.W + x0 + (m & (Wc - 1));
+        dv[k] = co_ok ? *reinterpret_cast<const f32x4*>(a.dy + pix * a.cout + co0 + 4 * cq) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int k = 0; k < WX_XI; ++k) {
+        const int y = y0 + xhy[k], x = x0 + xhx[k];
+        const bool ok = ci_ok && y >= 0 && y < a.H && x >= 0 && x < a.W;
+        xv[k] = ok ? *reinterpret_cast<const f32x4*>(a.x0 + ((img + y) * a.W + x) * cin + ci0 + 4 * cq)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    auto store = [&](_Float16* L) {
+#pragma unroll
+      for (int k = 0; k < WX_DI; ++k) {
+        const int m = (tid + 256 * k) >> 4;
+        wx_h4 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float x = dv[k][j];
+          asm volatile("" : "+v"(x));
+          const _Float16 hh = (_Float16)x;
+          hi[j] = hh;
+          lo[j] = (_Float16)(x - (float)hh);
+          gmax = fmaxf(gmax, fabsf(x));
+        }
+        const int o = wx_off(m, 4 * cq);
+        *(wx_lds_u2*)(L + o) = __builtin_bit_cast(wx_u2, hi);
+        *(wx_lds_u2*)(L + WX_PX * 64 + o) = __builtin_bit_cast(wx_u2, lo);
+      }
+      _Float16* X = L + WX_D;
+#pragma unroll
+      for (int k = 0; k < WX_XI; ++k) {
+        const int hp = (tid + 256 * k) >> 4;
+        if (hp < HP) {
+          wx_h4 hi, lo;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float x = xv[k][j];
+            asm volatile("" : "+v"(x));
+            const _Float16 hh = (_Float16)x;
+            hi[j] = hh;
+            lo[j] = (_Float16)(x - (float)hh);
+            gmax = fmaxf(gmax, fabsf(x));
+          }
+          const int o = wx_off(hp, 4 * cq);
+          *(wx_lds_u2*)(X + o) = __builtin_bit_cast(wx_u2, hi);
+          *(wx_lds_u2*)(X + WX_HMAX * 64 + o) = __builtin_bit_cast(wx_u2, lo);
+        }
+      }
+    };
+    // transposed-read lane roles: group G = lane >> 4 (G & 1: which 16 of the wave's 32 columns, G >> 1 = h:
+    // which 8 of the k-step's 16 pixels); lane 4q + p of the group addresses row q, columns 4p .. 4p + 3
+    const int G = lane >> 4, q = (lane & 15) >> 2, pcol = 4 * (lane & 3);
+    const int cA = wr + 16 * (G & 1) + pcol, cB = wc + 16 * (G & 1) + pcol;
+    load(c_beg);
+    for (int64_t c = c_beg; c < c_end; ++c) {
+      _Float16* L = lds[c & 1];
+      store(L);
+      __syncthreads();
+      if (c + 1 < c_end) load(c + 1);
+      const _Float16* Dh = L;
+      const _Float16* Dl = L + WX_PX * 64;
+      const _Float16* Xh = L + WX_D;
+      const _Float16* Xl = Xh + WX_HMAX * 64;
+#pragma unroll
+      for (int st = 0; st < WX_PX / 16; ++st) {
+        const int m0 = 16 * st + 8 * h;  // this lane-half's 8 pixels of the k-step: one row segment
+        const int oa0 = wx_off(m0 + q, cA), oa1 = wx_off(m0 + 4 + q, cA);
+        const wx_h4 ah0 = wx_tr(Dh, oa0), ah1 = wx_tr(Dh, oa1), al0 = wx_tr(Dl, oa0), al1 = wx_tr(Dl, oa1);
+        const wx_h8 ahi = {ah0[0], ah0[1], ah0[2], ah0[3], ah1[0], ah1[1], ah1[2], ah1[3]};
+        const wx_h8 alo = {al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
+        const int hb = (m0 >> lwc) * HWc + (m0 & (Wc - 1));
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int r0 = hb + (t / 3) * HWc + (t % 3);
+          const int ob0 = wx_off(r0 + q, cB), ob1 = wx_off(r0 + 4 + q, cB);
+          const wx_h4 bh0 = wx_tr(Xh, ob0), bh1 = wx_tr(Xh, ob1), bl0 = wx_tr(Xl, ob0), bl1 = wx_tr(Xl, ob1);
+          const wx_h8 bhi = {bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
+          const wx_h8 blo = {bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi, acc[t], 0, 0, 0);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (gmax >= 65504.0f) atomicOr(guard, 1u);
+  // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin][9]
+  float* slab = a.part + (size_t)blockIdx.y * a.cout * cin * 9;
+  const int ci = ci0 + wc + (lane & 31);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wr + 8 * (r >> 2) + 4 * h + (r & 3);
+      if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * 9 + t] = acc[t][r];
+    }
+}
+
 __global__ void slab_reduce_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out,
                                    int accumulate) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1119,6 +1306,45 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
     const int slices = (int)((P + slice - 1) / slice);
     if (!colpart || (int64_t)slices * cout > colpart_floats) {
       set_error("ifd_tr_conv_wgrad: column-sum workspace too small");
+      return 2;
+    }
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((cout + 63) / 64, slices), dim3(256), 0, s, dy, P, cout, slice,
+                       colpart);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((cout + 63) / 64), dim3(64), 0, s, colpart, slices, cout, db, 1);
+  }
+  return TR_LAST();
+}
+
+int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                         int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
+                         int64_t colpart_floats, unsigned* guard, void* stream) {
+  // the split kernel: 3x3, one input tensor, power-of-two maps >= 8 (wgrad9's chunking); else fp32
+  if (taps != 9 || c1 || H < 8 || (H & (H - 1)) || !guard)
+    return ifd_tr_conv_wgrad(dy, cout, x0, c0, x1, c1, N, H, taps, dw, db, part, part_floats, colpart, colpart_floats,
+                             stream);
+  const int64_t P = (int64_t)N * H * H;
+  int S = 1;
+  const int64_t need = ifd_tr_wgrad_part_floats(cout, c0, taps, P, &S);
+  if (!dy || !x0 || !dw || !part || need > part_floats) {
+    set_error("ifd_tr_conv_wgrad_x3: bad arguments or workspace too small");
+    return 2;
+  }
+  WgArgs a;
+  a.dy = dy; a.cout = cout; a.x0 = x0; a.c0 = c0; a.x1 = x0; a.c1 = 0;
+  a.N = N; a.H = H; a.W = H; a.taps = 9; a.P = P;
+  a.part = part;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nch = P / WX_PX;
+  a.chunks_per_split = (int)((nch + S - 1) / S);
+  const int tiles = ((cout + 63) / 64) * ((c0 + 63) / 64);
+  hipLaunchKernelGGL(wgrad_x3_kernel, dim3(tiles, S), dim3(256), 0, s, a, guard);
+  const int64_t n = (int64_t)cout * c0 * 9;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
+  if (db) {
+    const int64_t slice = colsum_slice(P);
+    const int slices = (int)((P + slice - 1) / slice);
+    if (!colpart || (int64_t)slices * cout > colpart_floats) {
+      set_error("ifd_tr_conv_wgrad_x3: column-sum workspace too small");
       return 2;
     }
     hipLaunchKernelGGL(colsum_partial_kernel, dim3((cout + 63) / 64, slices), dim3(256), 0, s, dy, P, cout, slice,

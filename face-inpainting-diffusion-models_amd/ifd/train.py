@@ -41,6 +41,7 @@ TRAIN_EXPORTS = {
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
     "ifd_tr_conv_wgrad": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp]),
+    "ifd_tr_conv_wgrad_x3": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp, vp]),
     "ifd_tr_gn_fwd": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_gn_bwd": (i32, [vp, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, i64, vp]),
     "ifd_tr_resample": (i32, [vp, i32, i32, i32, i32, vp, vp]),
@@ -96,19 +97,21 @@ class UNetTrainer:
 
     precision="3xf16": the 3x3 convs of the forward (and, with x3_dgrad, the dgrad convs of the backward)
     run on the sampler's fp32-accurate split kernel (conv_x3.hip: each fp32 operand = f16 hi + f16 lo,
-    three f16 MFMA products per MAC, fp32 accumulation). The backward then carries a loss scale of
+    three f16 MFMA products per MAC, fp32 accumulation); with x3_wgrad their weight gradients run on
+    wgrad_x3_kernel (both operands split on the fly, same arithmetic). The backward then carries a loss scale of
     2^x3_loss_scale_log2 (the eps-MSE gradient is ~1e-7 per element: below f16's normal range unscaled);
     every backward op is linear in the upstream gradient and the scale is a power of two, so removing it
     from the parameter gradients before clip + AdamW is exact. A split operand outside f16's range sets
     the range guard; the step is then recomputed in fp32 (same noise) with a warning. wgrad, GroupNorm,
-    attention, embeddings and the optimizer stay fp32."""
+    attention, embeddings, the 1x1 convs and the optimizer stay fp32."""
 
     def __init__(self, cfg: UNetConfig = FULL, device="cuda", lr=5e-5, weight_decay=0.01, betas=(0.9, 0.999),
-                 eps=1e-8, max_norm=1.0, precision="fp32", x3_dgrad=True, x3_loss_scale_log2=20):
+                 eps=1e-8, max_norm=1.0, precision="fp32", x3_dgrad=True, x3_wgrad=True, x3_loss_scale_log2=20):
         if precision not in ("fp32", "3xf16"):
             raise ValueError(f"precision must be 'fp32' or '3xf16', got {precision!r}")
         self.precision = precision
         self.x3_dgrad = bool(x3_dgrad)
+        self.x3_wgrad = bool(x3_wgrad)
         self.x3_loss_scale_log2 = int(x3_loss_scale_log2)
         self.guard_trips = 0
         self.cfg = cfg
@@ -254,8 +257,12 @@ class UNetTrainer:
         direct = real_cin == cin_x and real_cout == cout
         dw = self.g(name) if direct else self._zeros(cout * cin_x * taps)
         db = self.g(bias_name) if (bias_name and real_cout == cout) else (self._zeros(cout) if bias_name else None)
-        chk(lib().ifd_tr_conv_wgrad(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
-                                    P(colpart), colpart.numel(), self.s))
+        if self.precision == "3xf16" and self.x3_wgrad:
+            chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
+                                           P(colpart), colpart.numel(), P(self._guard), self.s))
+        else:
+            chk(lib().ifd_tr_conv_wgrad(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
+                                        P(colpart), colpart.numel(), self.s))
         if not direct:  # padded input (the first conv reads 16 channels, 9 real) or output (head: 8, 6 real)
             chk(lib().ifd_tr_copy_channels(P(dw), cin_x * taps, 0, P(self.g(name)), real_cin * taps, 0, real_cin * taps,
                                            real_cout, 1, self.s))
@@ -559,7 +566,7 @@ class UNetTrainer:
         chk(lib().ifd_tr_masked_mse(P(out6), cs, P(nc_), P(mc), N, H * W, P(self.loss), P(self._dout6), P(work),
                                     self.s))
         self._gscale = 1.0
-        if self._x3_active(True):
+        if self.precision == "3xf16" and (self.x3_dgrad or self.x3_wgrad):
             self._gscale = float(2.0 ** self.x3_loss_scale_log2)
             chk(lib().ifd_tr_scale(P(self._dout6), self._dout6.numel(), self._gscale, self.s))
         return self.loss
@@ -629,6 +636,7 @@ class BlockTrainer(UNetTrainer):
         self._zero_bias = torch.zeros(4096, device=self.dev)
         self._pack_cache = {}
         self.precision, self.x3_dgrad, self.x3_loss_scale_log2, self.guard_trips = "fp32", False, 0, 0
+        self.x3_wgrad = False
         self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
         self._grad_clean = False
         self._pack_cache = {}

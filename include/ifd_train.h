@@ -53,6 +53,12 @@ int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* sp
 int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                       int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
                       int64_t colpart_floats, void* stream);
+/* ifd_tr_conv_wgrad with the 3xf16 split kernel for 3x3 convs of one input tensor on maps >= 8x8 (both
+ * operands split on the fly, three f16 products per MAC, fp32 accumulation; |operand| >= 65504 sets bit 1
+ * of *guard); other shapes run ifd_tr_conv_wgrad. Same workspaces. */
+int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                         int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
+                         int64_t colpart_floats, unsigned* guard, void* stream);
 /* GroupNorm(32, C) (+ scale/shift: ss[n][0:C] = scale, ss[n][C:2C] = shift, row stride ss_stride) (+ SiLU).
  * stats[n][32][2] = (mean, rstd) saved for the backward; work: N * ceil(HW/256) * 64 doubles. */
 int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,

@@ -140,7 +140,7 @@ def _full_step(precision, B=4, scale_conv_in=1.0, **kw):
 
 
 def test_train_x3_full_matches_fp32(record):
-    """Full 256^2 config, B = 4: one 3xf16 step (forward + dgrad on the split kernel, loss scale 2^20)
+    """Full 256^2 config, B = 4: one 3xf16 step (forward, dgrad and wgrad on split kernels, loss scale 2^20)
     against the fp32 step from the same state, noise and GT-noise cache draw. Gates: loss relative 1e-5,
     global grad norm relative 1e-5, every parameter gradient ||g - g_fp32|| <= 1e-4 ||g_fp32|| (the fp32
     step vs the reference's own: <= 6e-6 on the reduced config), and no range-guard trip."""

@@ -12,7 +12,7 @@ from test_gpu_train import _full_step
 tr32, l32 = _full_step("fp32")
 g32 = tr32.grad.clone(); n32 = float(tr32.norm_coef[0]); offs = tr32.offsets
 del tr32
-for kw in (dict(x3_dgrad=False), dict(x3_loss_scale_log2=14), dict(x3_loss_scale_log2=20), dict(x3_loss_scale_log2=24)):
+for kw in (dict(x3_dgrad=False, x3_wgrad=False), dict(x3_wgrad=False), dict(x3_loss_scale_log2=14), dict(x3_loss_scale_log2=20), dict(x3_loss_scale_log2=24)):
     tr, l = _full_step("3xf16", **kw)
     errs = []
     for k, (o, shape) in offs.items():
