@@ -141,8 +141,8 @@ def spawn_ranks(n):
 def train_main(args):
     """`--workload train`: BASELINE configs[4]'s training step (code/train_inpainting.py:15-79), B images per GPU
     at 256x256: t ~ randint, training_losses with injection, backward, clip_grad_norm_(1.0), AdamW. Step = one
-    optimizer step. --precision 3xf16 (default): forward and dgrad 3x3 convs on the fp32-accurate split
-    kernel (ifd/train.py UNetTrainer precision="3xf16"); fp32: every conv on fp32 MFMA, as the reference
+    optimizer step. --precision 3xf16 (default): forward, dgrad and wgrad 3x3 convs on the fp32-accurate
+    split kernels (ifd/train.py UNetTrainer precision="3xf16"); fp32: every conv on fp32 MFMA, as the reference
     trains (no bf16 / LoRA exists in the reference). At N=1 the other mode is timed beside it.
     Multi-GPU: per-rank steps (data parallelism would add an all-reduce of the 374 MB gradient; not part of
     the reference, which trains on one device)."""
@@ -194,7 +194,7 @@ def train_main(args):
            "unit": "images/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None,
-           "dtype": "f32" if prec == "fp32" else "f32 (3xf16 split MFMA for the forward + dgrad 3x3 convs)",
+           "dtype": "f32" if prec == "fp32" else "f32 (3xf16 split MFMA for the forward, dgrad and wgrad 3x3 convs)",
            "data": "synthetic (gt~U(-1,1), rectangle masks, seeded weights)",
            "config": {"workload": "train_inpainting.py train_epoch step (BASELINE configs[4]; the reference trains "
                                   "fp32 and has no bf16/LoRA)", "global_batch": B * ws, "batch_per_gpu": B,
