@@ -113,6 +113,11 @@ bool conv_head_eligible(const ConvParams& p, int taps, int xform);
 size_t conv_head_pack_floats(int cin);
 void conv_head_pack(const float* w, int cout, int cin, float* dst);
 int launch_conv_head(const ConvParams& p, const float* wh, hipStream_t stream);
+// the same head on f16 MFMAs with split operands (3xf16 mode): weights packed by conv_head_x3_pack
+bool conv_head_x3_eligible(const ConvParams& p, int taps, int xform);
+size_t conv_head_x3_pack_floats(int cin);
+bool conv_head_x3_pack(const float* w, int cout, int cin, float* dst);
+int launch_conv_head_x3(const ConvParams& p, const float* wx, hipStream_t stream);
 
 // Shared elementwise step math, also used by the standalone step kernels (sampler.hip).
 __device__ __forceinline__ float ddim_step_value(const StepCoeffs& s, float img, float eps, float noise,

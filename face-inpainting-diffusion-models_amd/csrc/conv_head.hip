@@ -18,6 +18,8 @@
 // loads: at 27 KB they miss the scalar cache and every wait exposed its latency, 39 TFLOP/s.)
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "conv.h"
 #include "conv_dev.h"
 
@@ -177,6 +179,187 @@ __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const
   }
 }
 
+
+// ---- 3xf16 output head (the 3xf16 precision mode): the same conv on f16 MFMAs with split operands ----
+// The VALU head above reaches ~40 TFLOP/s (0.36 ms per eval at B = 16). Here a persistent block per CU
+// keeps ALL the head's split weights in LDS ([chunk][tap][part][16 co][32 ch] f16: 72 KiB for 128
+// channels, co 6..15 zero) and walks 16 x 16-pixel tiles: per 32-channel chunk the 256 threads stage
+// the activated, split 18 x 18 halo ([part][px][32 ch] f16), then wave w computes tile rows 4w..4w+3
+// as 16-pixel M blocks with v_mfma_f32_16x16x32_f16 (N = 16 output channels, 6 used), three split
+// products per MAC as conv_x3.hip (weights x 2^11). The next chunk's halo loads are in registers
+// while the MFMAs run. The epilogue transposes the accumulators through LDS so each thread finishes
+// one pixel with the VALU head's epilogue (bias, NCHW store or the fused DDIM / DDPM step).
+constexpr int HX_T = 16;                                  // tile 16 x 16
+constexpr int HX_HW = HX_T + 2, HX_NP = HX_HW * HX_HW;  // 324 halo pixels
+constexpr int HX_CH = 32;                                 // channels per chunk (one MFMA k-step)
+constexpr int HX_ITEMS = (HX_NP * 8 + 255) / 256;         // (pixel, quad) items per thread: 11
+constexpr int HX_MAXCH = 4;                               // chunks held in LDS (cin <= 128)
+constexpr int HX_WCH = 9 * 2 * 16 * HX_CH;                // f16 per chunk of packed weights
+constexpr int HX_A = 2 * HX_NP * HX_CH;                   // f16 per halo stage
+constexpr size_t HX_LDS = (size_t)(HX_MAXCH * HX_WCH + HX_A) * 2 + 256 * 8 * 4;
+typedef _Float16 hx_h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hx_h4 __attribute__((ext_vector_type(4)));
+typedef float hx_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned hx_u2 __attribute__((ext_vector_type(2)));
+
+template <int CO>
+__global__ __launch_bounds__(256, 1) void conv_head_x3_kernel(ConvParams p, const _Float16* __restrict__ wx) {
+  extern __shared__ __attribute__((aligned(16))) char hx_smem[];
+  _Float16* Wl = reinterpret_cast<_Float16*>(hx_smem);
+  _Float16* Al = Wl + HX_MAXCH * HX_WCH;
+  float* Ob = reinterpret_cast<float*>(Al + HX_A);  // [256 px][8]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cin = p.c0, nch = cin / HX_CH;
+  const int tiles_x = p.W / HX_T, tiles_y = p.H / HX_T;
+  const int ntiles = p.N * tiles_x * tiles_y;
+  // weights once per block
+  {
+    const hx_f4* src = reinterpret_cast<const hx_f4*>(wx);
+    hx_f4* dst = reinterpret_cast<hx_f4*>(Wl);
+    for (int i = tid; i < nch * HX_WCH / 8; i += 256) dst[i] = src[i];
+  }
+  const int q = tid & 7;  // channel quad of every staging item
+  int hyv[HX_ITEMS], hxv[HX_ITEMS];
+#pragma unroll
+  for (int k = 0; k < HX_ITEMS; ++k) {
+    const int px = (tid + 256 * k) >> 3;
+    hyv[k] = px < HX_NP ? px / HX_HW : -1000000;
+    hxv[k] = px % HX_HW;
+  }
+  hx_f4 raw[HX_ITEMS], ca, cb;
+  float gmax = 0.f;
+  auto tile_of = [&](int t, int& n, int& y0, int& x0) {
+    x0 = (t % tiles_x) * HX_T;
+    t /= tiles_x;
+    y0 = (t % tiles_y) * HX_T;
+    n = t / tiles_y;
+  };
+  auto load = [&](int t, int c) {
+    int n, y0, x0;
+    tile_of(t, n, y0, x0);
+    const float* src = p.in0 + (size_t)n * p.H * p.W * cin + HX_CH * c + 4 * q;
+#pragma unroll
+    for (int k = 0; k < HX_ITEMS; ++k) {
+      const int y = y0 + hyv[k] - 1, x = x0 + hxv[k] - 1;
+      const bool ok = y >= 0 && y < p.H && x >= 0 && x < p.W;
+      raw[k] = ok ? *reinterpret_cast<const hx_f4*>(src + ((size_t)y * p.W + x) * cin) : hx_f4{0.f, 0.f, 0.f, 0.f};
+    }
+    ca = hx_f4{1.f, 1.f, 1.f, 1.f};
+    cb = hx_f4{0.f, 0.f, 0.f, 0.f};
+    if (p.act != ACT_NONE) {
+      ca = *reinterpret_cast<const hx_f4*>(p.actA + (size_t)n * cin + HX_CH * c + 4 * q);
+      cb = *reinterpret_cast<const hx_f4*>(p.actB + (size_t)n * cin + HX_CH * c + 4 * q);
+    }
+  };
+  auto stage = [&](int t) {
+    int n, y0, x0;
+    tile_of(t, n, y0, x0);
+#pragma unroll
+    for (int k = 0; k < HX_ITEMS; ++k) {
+      const int px = (tid + 256 * k) >> 3;
+      if (px < HX_NP) {
+        const int y = y0 + hyv[k] - 1, x = x0 + hxv[k] - 1;
+        const bool ok = y >= 0 && y < p.H && x >= 0 && x < p.W;
+        hx_h4 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = raw[k][j];
+          if (p.act != ACT_NONE) {
+            v = ca[j] * v + cb[j];
+            if (p.act == ACT_AFFINE_SILU) v = silu_fast(v);
+          }
+          v = ok ? v : 0.f;  // zero padding of the activated input
+          asm volatile("" : "+v"(v));
+          gmax = fmaxf(gmax, fabsf(v));
+          const _Float16 hh = (_Float16)v;
+          hi[j] = hh;
+          lo[j] = (_Float16)(v - (float)hh);
+        }
+        *reinterpret_cast<hx_u2*>(Al + px * HX_CH + 4 * q) = __builtin_bit_cast(hx_u2, hi);
+        *reinterpret_cast<hx_u2*>(Al + HX_NP * HX_CH + px * HX_CH + 4 * q) = __builtin_bit_cast(hx_u2, lo);
+      }
+    }
+  };
+  // MFMA lane roles (16x16x32): A lane = pixel i (lane & 15) of a tile row, K group kg = lane >> 4
+  // (channels 8 kg .. 8 kg + 7); B lane = output channel j (lane & 15), same K group; C lane = channel
+  // j, pixels 4 kg .. 4 kg + 3 of the row
+  const int li = lane & 15, kg = lane >> 4;
+  const int nwork = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  if (nwork > 0) load(blockIdx.x, 0);
+  for (int u = 0; u < nwork; ++u) {
+    const int t = blockIdx.x + u * gridDim.x;
+    hx_f4 acc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = hx_f4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nch; ++c) {
+      __syncthreads();  // previous chunk's MFMA reads (and the weight copy) done
+      stage(t);
+      __syncthreads();
+      // next chunk's (or next tile's first chunk's) loads in flight during the MFMAs
+      if (c + 1 < nch)
+        load(t, c + 1);
+      else if (u + 1 < nwork)
+        load(t + gridDim.x, 0);
+      const _Float16* Wc = Wl + c * HX_WCH;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ky = tap / 3, kx = tap % 3;
+        const hx_h8 bh = *reinterpret_cast<const hx_h8*>(Wc + ((tap * 2 + 0) * 16 + li) * HX_CH + 8 * kg);
+        const hx_h8 bl = *reinterpret_cast<const hx_h8*>(Wc + ((tap * 2 + 1) * 16 + li) * HX_CH + 8 * kg);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int hp = (4 * wave + r + ky) * HX_HW + li + kx;
+          const hx_h8 ah = *reinterpret_cast<const hx_h8*>(Al + hp * HX_CH + 8 * kg);
+          const hx_h8 al = *reinterpret_cast<const hx_h8*>(Al + HX_NP * HX_CH + hp * HX_CH + 8 * kg);
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[r], 0, 0, 0);
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[r], 0, 0, 0);
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[r], 0, 0, 0);
+        }
+      }
+    }
+    // transpose: Ob[pixel][channel], pixel = tile row (4 wave + r) x 16 + column (4 kg + e)
+    if (li < 8)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Ob[((4 * wave + r) * HX_T + 4 * kg + e) * 8 + li] = acc[r][e] * (1.0f / 2048.0f);
+    __syncthreads();
+    {
+      int n, y0, x0;
+      tile_of(t, n, y0, x0);
+      const int HWp = p.H * p.W;
+      const size_t pix = (size_t)(y0 + (tid >> 4)) * p.W + (x0 + (tid & 15));
+      float a[8];
+#pragma unroll
+      for (int co = 0; co < 8; ++co) a[co] = Ob[tid * 8 + co];
+      if (p.epi == EPI_NCHW) {
+#pragma unroll
+        for (int co = 0; co < CO; ++co) p.out[((size_t)n * CO + co) * HWp + pix] = a[co] + p.bias[co];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const size_t o3 = ((size_t)n * 3 + c) * HWp + pix;
+          const size_t om = (size_t)n * HWp + pix;
+          const float eps = a[c] + p.bias[c];
+          const float x = p.img[o3];
+          const float mk = p.sc.inject ? p.mask[om] : 0.f;
+          const float g = p.sc.inject ? p.gt[o3] : 0.f;
+          const float kn = p.sc.inject ? p.known[o3] : 0.f;
+          float v;
+          if (p.epi == EPI_DDIM) {
+            const float nz = p.sc.use_noise ? p.noise[o3] : 0.f;
+            v = ddim_step_value(p.sc, x, eps, nz, g, mk, kn);
+          } else {
+            const float var_v = a[CO > 3 ? c + 3 : c] + p.bias[c + 3];
+            v = ddpm_step_value(p.sc, x, eps, var_v, p.noise[o3], g, mk, kn);
+          }
+          p.img[o3] = v;
+        }
+      }
+    }
+  }
+  if (p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
+}
 }  // namespace
 
 bool conv_head_eligible(const ConvParams& p, int taps, int xform) {
@@ -204,6 +387,62 @@ int launch_conv_head(const ConvParams& p, const float* wh, hipStream_t stream) {
     hipLaunchKernelGGL(conv_head_kernel<6>, dim3(blocks), dim3(HD_NT), 0, stream, p, wh);
   else
     hipLaunchKernelGGL(conv_head_kernel<3>, dim3(blocks), dim3(HD_NT), 0, stream, p, wh);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ifd
+
+namespace ifd {
+
+bool conv_head_x3_eligible(const ConvParams& p, int taps, int xform) {
+  return conv_head_eligible(p, taps, xform) && p.c0 % HX_CH == 0 && p.c0 <= HX_MAXCH * HX_CH && p.H % HX_T == 0 &&
+         p.W % HX_T == 0;
+}
+
+size_t conv_head_x3_pack_floats(int cin) { return (size_t)(cin / HX_CH) * HX_WCH / 2; }
+
+// w: [cout][cin][3][3] -> [cin/32][tap][part][16 co][32 ch] f16: part 0 = f16(w) 2^11, part 1 =
+// f16((w - f16(w)) 2^11) (conv_x3.hip's weight split); false if |w| >= 32 (the head then stays fp32)
+bool conv_head_x3_pack(const float* w, int cout, int cin, float* dst_f) {
+  _Float16* dst = reinterpret_cast<_Float16*>(dst_f);
+  bool ok = true;
+  for (int ch = 0; ch < cin / HX_CH; ++ch)
+    for (int tap = 0; tap < 9; ++tap)
+      for (int part = 0; part < 2; ++part)
+        for (int co = 0; co < 16; ++co)
+          for (int c = 0; c < HX_CH; ++c) {
+            const float v = co < cout ? w[((size_t)co * cin + ch * HX_CH + c) * 9 + tap] : 0.f;
+            const _Float16 hi = (_Float16)v;
+            _Float16 o;
+            if (part == 0) {
+              const float sc = (float)hi * 2048.0f;
+              if (!(std::fabs(sc) <= 65504.0f)) ok = false;
+              o = (_Float16)sc;
+            } else {
+              o = (_Float16)((v - (float)hi) * 2048.0f);
+            }
+            dst[((((size_t)ch * 9 + tap) * 2 + part) * 16 + co) * HX_CH + c] = o;
+          }
+  return ok;
+}
+
+int launch_conv_head_x3(const ConvParams& p, const float* wx, hipStream_t stream) {
+  const int ntiles = p.N * (p.H / HX_T) * (p.W / HX_T);
+  const int ncu = device_cu_count();
+  const int grid = ntiles < ncu ? ntiles : ncu;
+  if (p.cout == 6) {
+    static bool attr_set[kMaxDevices] = {};
+    hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_head_x3_kernel<6>), (int)HX_LDS);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(conv_head_x3_kernel<6>, dim3(grid), dim3(256), HX_LDS, stream, p,
+                       reinterpret_cast<const _Float16*>(wx));
+  } else {
+    static bool attr_set[kMaxDevices] = {};
+    hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_head_x3_kernel<3>), (int)HX_LDS);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(conv_head_x3_kernel<3>, dim3(grid), dim3(256), HX_LDS, stream, p,
+                       reinterpret_cast<const _Float16*>(wx));
+  }
   return (int)hipGetLastError();
 }
 

@@ -347,8 +347,12 @@ __device__ __forceinline__ wx_h4 wx_tr(const _Float16* L, int off) {
   return __builtin_bit_cast(wx_h4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) wx_hv4*)(L + off)));
 }
 
-__global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard) {
+// colpart (optional): the bias gradient's column sums of dY, fused: the ci-tile-0 blocks add their
+// split's pixels per channel (fixed order: per thread over chunks, then the 16 pixel lanes in lane
+// order) into colpart[split][cout]; colsum_final_kernel adds the splits in order.
+__global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
+  __shared__ f32x4 csred[256];
   const int cin = a.c0;
   const int nci = (cin + 63) / 64;
   const int cit = blockIdx.x % nci, cot = blockIdx.x / nci;
@@ -369,6 +373,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   float gmax = 0.f;
+  const bool do_cs = colpart && cit == 0;
+  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
   if (c_beg < c_end) {
     // staging items: (pixel i >> 4, channel quad i & 15), i = tid + 256 k; quad fixed per thread
     const int cq = tid & 15;
@@ -408,6 +414,9 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
       }
     };
     auto store = [&](_Float16* L) {
+      if (do_cs)
+#pragma unroll
+        for (int k = 0; k < WX_DI; ++k) csum += dv[k];
 #pragma unroll
       for (int k = 0; k < WX_DI; ++k) {
         const int m = (tid + 256 * k) >> 4;
@@ -484,6 +493,19 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
     }
   }
   if (gmax >= 65504.0f) atomicOr(guard, 1u);
+  if (do_cs) {  // (block-uniform)
+    csred[tid] = csum;
+    __syncthreads();
+    if (tid < 16) {
+      f32x4 t = csred[tid];
+      for (int r = 1; r < 16; ++r) t += csred[tid + 16 * r];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = co0 + 4 * tid + j;
+        if (co < a.cout) colpart[(size_t)blockIdx.y * a.cout + co] = t[j];
+      }
+    }
+  }
   // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin][9]
   float* slab = a.part + (size_t)blockIdx.y * a.cout * cin * 9;
   const int ci = ci0 + wc + (lane & 31);
@@ -1337,10 +1359,14 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   const int64_t nch = P / WX_PX;
   a.chunks_per_split = (int)((nch + S - 1) / S);
   const int tiles = ((cout + 63) / 64) * ((c0 + 63) / 64);
-  hipLaunchKernelGGL(wgrad_x3_kernel, dim3(tiles, S), dim3(256), 0, s, a, guard);
+  // bias gradient fused into the kernel when the column-sum workspace holds one row per split
+  const bool fused_db = db && colpart && (int64_t)S * cout <= colpart_floats && cout % 4 == 0;
+  hipLaunchKernelGGL(wgrad_x3_kernel, dim3(tiles, S), dim3(256), 0, s, a, guard, fused_db ? colpart : nullptr);
   const int64_t n = (int64_t)cout * c0 * 9;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
-  if (db) {
+  if (fused_db) {
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((cout + 63) / 64), dim3(64), 0, s, colpart, S, cout, db, 1);
+  } else if (db) {
     const int64_t slice = colsum_slice(P);
     const int slices = (int)((P + slice - 1) / slice);
     if (!colpart || (int64_t)slices * cout > colpart_floats) {

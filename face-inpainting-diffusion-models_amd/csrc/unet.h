@@ -19,6 +19,8 @@ struct ConvW {
   size_t x3s_off = 0;  // ... of the 1x1 skip segment
   bool x3_ok = false;  // every weight within the split's range (|w| < 32): the layer may run 3xf16
   size_t head_off = 0;  // float offset of the output-head packing (conv_head.hip), 0 if none
+  size_t head_x3_off = 0;  // the 3xf16 head's split packing (conv_head_x3_pack), 0 if none
+  bool head_x3_ok = false;  // every head weight within the split's range
   std::string wname, bname, swname, sbname;  // source parameter names
 };
 
@@ -155,7 +157,8 @@ class Model {
   std::map<const float*, StatRec> stat_;
   bool gn_fused_ = true;
   int opt_stream_ = 2;      // wide fp32 layers: 0 one tile per workgroup, 1/2 persistent (1 or 2 per CU)
-  int opt_x3_off_ = 0;      // bisecting mask: 1 no 16x16 tiles, 2 no split-K, 4 no skip layers, 8 no 8x8, 16 no 1x1
+  int opt_x3_off_ = 0;      // bisecting mask: 1 no 16x16 tiles, 2 no split-K, 4 no skip layers, 8 no 8x8, 16 no 1x1,
+                            // 32 no split-MFMA output head
   int opt_stream_cw_ = 8;   // conv_stream consumer waves (4 or 8)
   int opt_bm128_ = 0;       // 128-pixel fp32 tiles only
   int opt_lds_pad_ = 0;     // extra LDS bytes per fp32 conv block

@@ -493,6 +493,9 @@ int Model::finalize() {
   conv_out_.head_off = 0;
   if (conv_out_.taps == 9 && conv_out_.cin % 16 == 0 && (conv_out_.cout == 6 || conv_out_.cout == 3))
     conv_out_.head_off = reserve(conv_head_pack_floats(conv_out_.cin));
+  conv_out_.head_x3_off = 0;
+  if (conv_out_.head_off && conv_out_.cin % 32 == 0 && conv_out_.cin <= 128)
+    conv_out_.head_x3_off = reserve(conv_head_x3_pack_floats(conv_out_.cin));
 
   std::vector<float> blob(n, 0.f);
   auto put = [&](size_t off, const std::vector<float>& v) { std::copy(v.begin(), v.end(), blob.begin() + off); };
@@ -561,6 +564,9 @@ int Model::finalize() {
   fill_conv(conv_out_);
   if (conv_out_.head_off)
     conv_head_pack(host_[conv_out_.wname].data(), conv_out_.cout, conv_out_.cin, blob.data() + conv_out_.head_off);
+  conv_out_.head_x3_ok = conv_out_.head_x3_off &&
+                         conv_head_x3_pack(host_[conv_out_.wname].data(), conv_out_.cout, conv_out_.cin,
+                                           blob.data() + conv_out_.head_x3_off);
 
   if (wblob_) IFD_CHECK_HIP(hipFree(wblob_));
   wblob_ = nullptr;
@@ -731,7 +737,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   // act(GN(x)) materialised first when the conv has a prologue (act_apply, the conv prologue's
   // fp32 arithmetic)
   // development option x3_off (bisecting): 1 no 16x16 tiles, 2 no split-K, 4 no skip layers,
-  // 8 no 8x8 four-image tiles, 16 no 1x1-only launches
+  // 8 no 8x8 four-image tiles, 16 no 1x1-only launches, 32 no split-MFMA output head
   const int x3_off = opt_x3_off_;
   auto x3_masked_for = [&](const ConvParams& g) {
     return ((x3_off & 1) && g.TW == 16) || ((x3_off & 2) && g.ksplit > 1) || ((x3_off & 4) && cw.has_skip) ||
@@ -810,8 +816,10 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   } else if (x3_geo) {  // not split-eligible after all: the fp32 kernels' own geometry
     conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8);
   }
-  // the output head (cout 6): fp32 VALU kernel in every precision mode
+  // the output head (cout 6): fp32 VALU kernel, or in the 3xf16 mode the split-MFMA head
   const bool use_head = !use_x3 && cw.head_off && conv_head_eligible(p, cw.taps, xf);
+  const bool use_head_x3 = use_head && prec_ == IFD_PREC_3XF16 && cw.head_x3_ok && !(opt_x3_off_ & 32) &&
+                           conv_head_x3_eligible(p, cw.taps, xf);
   const bool use_stream = !use_head && (use_x3 || (stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn)));
   // fused GroupNorm statistics of the output (single-image tiles, no split-K; not mode 1)
   p.gstat = nullptr;
@@ -861,6 +869,8 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
     else if (use_x3)
       snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d,%d>", xf, cw.has_skip ? "true" : "false", p.TW, p.x3_nprod);
+    else if (use_head_x3)
+      snprintf(nm, sizeof(nm), "conv_head_x3_kernel<%d>", cw.cout);
     else if (use_head)
       snprintf(nm, sizeof(nm), "conv_head_kernel<%d>", cw.cout);
     else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
@@ -875,6 +885,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   prof_begin(s, &e0, nm);
   if (use_head) p.ksplit = 1;
   int e = use_x3       ? launch_conv_x3(p, xf, s)
+          : use_head_x3 ? launch_conv_head_x3(p, wblob_ + cw.head_x3_off, s)
           : use_head   ? launch_conv_head(p, wblob_ + cw.head_off, s)
           : use_stream ? launch_conv_stream(p, xf, stream_mode, s)
                        : launch_conv(p, cw.taps, xf, cw.bn, s);
