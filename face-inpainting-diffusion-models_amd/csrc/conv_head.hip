@@ -181,9 +181,9 @@ __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const
 
 
 // ---- 3xf16 output head (the 3xf16 precision mode): the same conv on f16 MFMAs with split operands ----
-// The VALU head above reaches ~40 TFLOP/s (0.36 ms per eval at B = 16). Here a persistent block per CU
-// keeps ALL the head's split weights in LDS ([chunk][tap][part][16 co][32 ch] f16: 72 KiB for 128
-// channels, co 6..15 zero) and walks 16 x 16-pixel tiles: per 32-channel chunk the 256 threads stage
+// The VALU head above reaches ~40 TFLOP/s (0.36 ms per eval at B = 16). Here persistent blocks (two
+// per CU) keep ALL the head's split weights in LDS ([chunk][tap][part][8 co][32 ch] f16: 36 KiB for
+// 128 channels, co 6, 7 zero) and walk 16 x 16-pixel tiles: per 32-channel chunk the 256 threads stage
 // the activated, split 18 x 18 halo ([part][px][32 ch] f16), then wave w computes tile rows 4w..4w+3
 // as 16-pixel M blocks with v_mfma_f32_16x16x32_f16 (N = 16 output channels, 6 used), three split
 // products per MAC as conv_x3.hip (weights x 2^11). The next chunk's halo loads are in registers
@@ -194,20 +194,26 @@ constexpr int HX_HW = HX_T + 2, HX_NP = HX_HW * HX_HW;  // 324 halo pixels
 constexpr int HX_CH = 32;                                 // channels per chunk (one MFMA k-step)
 constexpr int HX_ITEMS = (HX_NP * 8 + 255) / 256;         // (pixel, quad) items per thread: 11
 constexpr int HX_MAXCH = 4;                               // chunks held in LDS (cin <= 128)
-constexpr int HX_WCH = 9 * 2 * 16 * HX_CH;                // f16 per chunk of packed weights
+constexpr int HX_WCO = 8;                                 // packed output channels (6 used; B lanes 8..15 read zeros)
+constexpr int HX_WCH = 9 * 2 * HX_WCO * HX_CH;            // f16 per chunk of packed weights
 constexpr int HX_A = 2 * HX_NP * HX_CH;                   // f16 per halo stage
-constexpr size_t HX_LDS = (size_t)(HX_MAXCH * HX_WCH + HX_A) * 2 + 256 * 8 * 4;
+constexpr int HX_Z = 32;                                  // a zero row for the unused B lanes
+// weights + zero row + halo stage (the epilogue's transpose buffer reuses the halo stage): 78.4 KiB,
+// two blocks per CU
+constexpr size_t HX_LDS = (size_t)(HX_MAXCH * HX_WCH + HX_Z + HX_A) * 2;
+static_assert(256 * 8 * 4 <= HX_A * 2, "transpose buffer fits the halo stage");
 typedef _Float16 hx_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 hx_h4 __attribute__((ext_vector_type(4)));
 typedef float hx_f4 __attribute__((ext_vector_type(4)));
 typedef unsigned hx_u2 __attribute__((ext_vector_type(2)));
 
 template <int CO>
-__global__ __launch_bounds__(256, 1) void conv_head_x3_kernel(ConvParams p, const _Float16* __restrict__ wx) {
+__global__ __launch_bounds__(256, 2) void conv_head_x3_kernel(ConvParams p, const _Float16* __restrict__ wx) {
   extern __shared__ __attribute__((aligned(16))) char hx_smem[];
   _Float16* Wl = reinterpret_cast<_Float16*>(hx_smem);
-  _Float16* Al = Wl + HX_MAXCH * HX_WCH;
-  float* Ob = reinterpret_cast<float*>(Al + HX_A);  // [256 px][8]
+  _Float16* Zl = Wl + HX_MAXCH * HX_WCH;
+  _Float16* Al = Zl + HX_Z;
+  float* Ob = reinterpret_cast<float*>(Al);  // [256 px][8], after the tile's last MFMAs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = p.c0, nch = cin / HX_CH;
   const int tiles_x = p.W / HX_T, tiles_y = p.H / HX_T;
@@ -217,6 +223,7 @@ __global__ __launch_bounds__(256, 1) void conv_head_x3_kernel(ConvParams p, cons
     const hx_f4* src = reinterpret_cast<const hx_f4*>(wx);
     hx_f4* dst = reinterpret_cast<hx_f4*>(Wl);
     for (int i = tid; i < nch * HX_WCH / 8; i += 256) dst[i] = src[i];
+    if (tid < HX_Z / 8) reinterpret_cast<hx_f4*>(Zl)[tid] = hx_f4{0.f, 0.f, 0.f, 0.f};
   }
   const int q = tid & 7;  // channel quad of every staging item
   int hyv[HX_ITEMS], hxv[HX_ITEMS];
@@ -301,23 +308,37 @@ __global__ __launch_bounds__(256, 1) void conv_head_x3_kernel(ConvParams p, cons
       else if (u + 1 < nwork)
         load(t + gridDim.x, 0);
       const _Float16* Wc = Wl + c * HX_WCH;
+      // per kernel column kx: the 6 halo rows the wave's 4 tile rows need (A), then the 3 taps (ky) of
+      // the column; one column's fragments at a time keeps the live set within two waves per SIMD
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int ky = tap / 3, kx = tap % 3;
-        const hx_h8 bh = *reinterpret_cast<const hx_h8*>(Wc + ((tap * 2 + 0) * 16 + li) * HX_CH + 8 * kg);
-        const hx_h8 bl = *reinterpret_cast<const hx_h8*>(Wc + ((tap * 2 + 1) * 16 + li) * HX_CH + 8 * kg);
+      for (int kx = 0; kx < 3; ++kx) {
+        hx_h8 ah[6], al[6];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int hp = (4 * wave + r + ky) * HX_HW + li + kx;
-          const hx_h8 ah = *reinterpret_cast<const hx_h8*>(Al + hp * HX_CH + 8 * kg);
-          const hx_h8 al = *reinterpret_cast<const hx_h8*>(Al + HX_NP * HX_CH + hp * HX_CH + 8 * kg);
-          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[r], 0, 0, 0);
-          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc[r], 0, 0, 0);
-          acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc[r], 0, 0, 0);
+        for (int rr = 0; rr < 6; ++rr) {
+          const int hp = (4 * wave + rr) * HX_HW + li + kx;
+          ah[rr] = *reinterpret_cast<const hx_h8*>(Al + hp * HX_CH + 8 * kg);
+          al[rr] = *reinterpret_cast<const hx_h8*>(Al + HX_NP * HX_CH + hp * HX_CH + 8 * kg);
         }
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int tap = 3 * ky + kx;
+          const _Float16* bp0 = li < HX_WCO ? Wc + ((tap * 2 + 0) * HX_WCO + li) * HX_CH + 8 * kg : Zl;
+          const _Float16* bp1 = li < HX_WCO ? Wc + ((tap * 2 + 1) * HX_WCO + li) * HX_CH + 8 * kg : Zl;
+          const hx_h8 bh = *reinterpret_cast<const hx_h8*>(bp0);
+          const hx_h8 bl = *reinterpret_cast<const hx_h8*>(bp1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bh, acc[r], 0, 0, 0);
+            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bl, acc[r], 0, 0, 0);
+            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[r + ky], bh, acc[r], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    // transpose: Ob[pixel][channel], pixel = tile row (4 wave + r) x 16 + column (4 kg + e)
+    // transpose: Ob[pixel][channel], pixel = tile row (4 wave + r) x 16 + column (4 kg + e); Ob is the
+    // halo stage, so every wave's MFMA reads must be done first
+    __syncthreads();
     if (li < 8)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -401,7 +422,7 @@ bool conv_head_x3_eligible(const ConvParams& p, int taps, int xform) {
 
 size_t conv_head_x3_pack_floats(int cin) { return (size_t)(cin / HX_CH) * HX_WCH / 2; }
 
-// w: [cout][cin][3][3] -> [cin/32][tap][part][16 co][32 ch] f16: part 0 = f16(w) 2^11, part 1 =
+// w: [cout][cin][3][3] -> [cin/32][tap][part][8 co][32 ch] f16: part 0 = f16(w) 2^11, part 1 =
 // f16((w - f16(w)) 2^11) (conv_x3.hip's weight split); false if |w| >= 32 (the head then stays fp32)
 bool conv_head_x3_pack(const float* w, int cout, int cin, float* dst_f) {
   _Float16* dst = reinterpret_cast<_Float16*>(dst_f);
@@ -409,7 +430,7 @@ bool conv_head_x3_pack(const float* w, int cout, int cin, float* dst_f) {
   for (int ch = 0; ch < cin / HX_CH; ++ch)
     for (int tap = 0; tap < 9; ++tap)
       for (int part = 0; part < 2; ++part)
-        for (int co = 0; co < 16; ++co)
+        for (int co = 0; co < HX_WCO; ++co)
           for (int c = 0; c < HX_CH; ++c) {
             const float v = co < cout ? w[((size_t)co * cin + ch * HX_CH + c) * 9 + tap] : 0.f;
             const _Float16 hi = (_Float16)v;
@@ -421,14 +442,14 @@ bool conv_head_x3_pack(const float* w, int cout, int cin, float* dst_f) {
             } else {
               o = (_Float16)((v - (float)hi) * 2048.0f);
             }
-            dst[((((size_t)ch * 9 + tap) * 2 + part) * 16 + co) * HX_CH + c] = o;
+            dst[((((size_t)ch * 9 + tap) * 2 + part) * HX_WCO + co) * HX_CH + c] = o;
           }
   return ok;
 }
 
 int launch_conv_head_x3(const ConvParams& p, const float* wx, hipStream_t stream) {
   const int ntiles = p.N * (p.H / HX_T) * (p.W / HX_T);
-  const int ncu = device_cu_count();
+  const int ncu = 2 * device_cu_count();  // two blocks per CU
   const int grid = ntiles < ncu ? ntiles : ncu;
   if (p.cout == 6) {
     static bool attr_set[kMaxDevices] = {};

@@ -350,7 +350,10 @@ __device__ __forceinline__ wx_h4 wx_tr(const _Float16* L, int off) {
 // colpart (optional): the bias gradient's column sums of dY, fused: the ci-tile-0 blocks add their
 // split's pixels per channel (fixed order: per thread over chunks, then the 16 pixel lanes in lane
 // order) into colpart[split][cout]; colsum_final_kernel adds the splits in order.
+// TAPS = 9 (3x3, halo of one pixel) or 1 (1x1: the chunk's own pixels, no halo).
+template <int TAPS>
 __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
+  constexpr int HALO = TAPS == 9 ? 1 : 0;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
   __shared__ f32x4 csred[256];
   const int cin = a.c0;
@@ -361,15 +364,15 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
   const int h = lane >> 5;
   const int wr = 32 * (wave & 1), wc = 32 * (wave >> 1);
   const int Wc = a.W < 32 ? a.W : 32, R = WX_PX / Wc;
-  const int HWc = Wc + 2, HP = (R + 2) * HWc;
+  const int HWc = Wc + 2 * HALO, HP = (R + 2 * HALO) * HWc;
   const int lwc = __builtin_ctz(Wc);
   const int segs = a.W / Wc, rows_per_img = a.H / R;
   const int64_t nch = (int64_t)a.N * rows_per_img * segs;
   const int64_t c_beg = (int64_t)blockIdx.y * a.chunks_per_split;
   const int64_t c_end = c_beg + a.chunks_per_split < nch ? c_beg + a.chunks_per_split : nch;
-  f32x16 acc[9];
+  f32x16 acc[TAPS];
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int t = 0; t < TAPS; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   float gmax = 0.f;
@@ -384,8 +387,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
 #pragma unroll
     for (int k = 0; k < WX_XI; ++k) {
       const int hp = (tid + 256 * k) >> 4;
-      xhy[k] = hp < HP ? hp / HWc - 1 : -1000000;  // halo row / column relative to the chunk origin
-      xhx[k] = hp % HWc - 1;
+      xhy[k] = hp < HP ? hp / HWc - HALO : -1000000;  // halo row / column relative to the chunk origin
+      xhx[k] = hp % HWc - HALO;
     }
     auto chunk_origin = [&](int64_t c, int& n, int& y0, int& x0) {
       const int64_t per_img = (int64_t)rows_per_img * segs;
@@ -478,8 +481,8 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
         const wx_h8 alo = {al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
         const int hb = (m0 >> lwc) * HWc + (m0 & (Wc - 1));
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int r0 = hb + (t / 3) * HWc + (t % 3);
+        for (int t = 0; t < TAPS; ++t) {
+          const int r0 = TAPS == 9 ? hb + (t / 3) * HWc + (t % 3) : hb;
           const int ob0 = wx_off(r0 + q, cB), ob1 = wx_off(r0 + 4 + q, cB);
           const wx_h4 bh0 = wx_tr(Xh, ob0), bh1 = wx_tr(Xh, ob1), bl0 = wx_tr(Xl, ob0), bl1 = wx_tr(Xl, ob1);
           const wx_h8 bhi = {bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
@@ -506,15 +509,15 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
       }
     }
   }
-  // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin][9]
-  float* slab = a.part + (size_t)blockIdx.y * a.cout * cin * 9;
+  // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin][TAPS]
+  float* slab = a.part + (size_t)blockIdx.y * a.cout * cin * TAPS;
   const int ci = ci0 + wc + (lane & 31);
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int t = 0; t < TAPS; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + wr + 8 * (r >> 2) + 4 * h + (r & 3);
-      if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * 9 + t] = acc[t][r];
+      if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * TAPS + t] = acc[t][r];
     }
 }
 
@@ -1340,8 +1343,8 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
 int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                          int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
                          int64_t colpart_floats, unsigned* guard, void* stream) {
-  // the split kernel: 3x3, one input tensor, power-of-two maps >= 8 (wgrad9's chunking); else fp32
-  if (taps != 9 || c1 || H < 8 || (H & (H - 1)) || !guard)
+  // the split kernel: 3x3 or 1x1, one input tensor, power-of-two maps >= 8; else fp32
+  if ((taps != 9 && taps != 1) || c1 || H < 8 || (H & (H - 1)) || !guard)
     return ifd_tr_conv_wgrad(dy, cout, x0, c0, x1, c1, N, H, taps, dw, db, part, part_floats, colpart, colpart_floats,
                              stream);
   const int64_t P = (int64_t)N * H * H;
@@ -1353,7 +1356,7 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   }
   WgArgs a;
   a.dy = dy; a.cout = cout; a.x0 = x0; a.c0 = c0; a.x1 = x0; a.c1 = 0;
-  a.N = N; a.H = H; a.W = H; a.taps = 9; a.P = P;
+  a.N = N; a.H = H; a.W = H; a.taps = taps; a.P = P;
   a.part = part;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nch = P / WX_PX;
@@ -1361,8 +1364,11 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   const int tiles = ((cout + 63) / 64) * ((c0 + 63) / 64);
   // bias gradient fused into the kernel when the column-sum workspace holds one row per split
   const bool fused_db = db && colpart && (int64_t)S * cout <= colpart_floats && cout % 4 == 0;
-  hipLaunchKernelGGL(wgrad_x3_kernel, dim3(tiles, S), dim3(256), 0, s, a, guard, fused_db ? colpart : nullptr);
-  const int64_t n = (int64_t)cout * c0 * 9;
+  if (taps == 9)
+    hipLaunchKernelGGL(wgrad_x3_kernel<9>, dim3(tiles, S), dim3(256), 0, s, a, guard, fused_db ? colpart : nullptr);
+  else
+    hipLaunchKernelGGL(wgrad_x3_kernel<1>, dim3(tiles, S), dim3(256), 0, s, a, guard, fused_db ? colpart : nullptr);
+  const int64_t n = (int64_t)cout * c0 * taps;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (fused_db) {
     hipLaunchKernelGGL(colsum_final_kernel, dim3((cout + 63) / 64), dim3(64), 0, s, colpart, S, cout, db, 1);
