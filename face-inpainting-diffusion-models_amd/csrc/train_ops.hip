@@ -1148,6 +1148,42 @@ __global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int c
   dst[((base + 2 + hh) * 64 + col) * 8 + j] = lo;
 }
 
+// 3xf16 packing of a 1x1 conv weight for the split kernel's 1x1 chunks (unet.hip pack_skip_x3's layout:
+// [cout_pad/64][cin/32][q][part][h][64][8] f16, element (q, part, h, col, j) of chunk s = split part of
+// W[64 ct + col][32 s + 16 h + 8 q + j]); transpose=1 packs the dgrad conv (out = cin, in = cout).
+__global__ void pack_conv1x1_x3_kernel(const float* __restrict__ w, int cout, int cin, int cs_pad, int cout_pad,
+                                       int transpose, _Float16* __restrict__ dst, unsigned* guard) {
+#pragma clang fp contract(off)
+  const int ns = cs_pad / 32;
+  const int64_t tot = (int64_t)(cout_pad / 64) * ns * 2 * 2 * 64 * 8;  // without the part index
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int j = (int)(i & 7);
+  int64_t r = i >> 3;
+  const int col = (int)(r & 63);
+  r >>= 6;
+  const int hh = (int)(r & 1);
+  r >>= 1;
+  const int qq = (int)(r & 1);
+  r >>= 1;
+  const int sk = (int)(r % ns);
+  const int ct = (int)(r / ns);
+  const int o = ct * 64 + col, c = sk * 32 + hh * 16 + qq * 8 + j;
+  float v = 0.f;
+  if (transpose == 0) {
+    if (o < cout && c < cin) v = w[(size_t)o * cin + c];
+  } else {
+    if (o < cin && c < cout) v = w[(size_t)c * cin + o];
+  }
+  const _Float16 hi = (_Float16)v;
+  const float sc = (float)hi * 2048.0f;
+  if (!(fabsf(sc) <= 65504.0f)) atomicOr(guard, 2u);
+  const _Float16 lo = (_Float16)((v - (float)hi) * 2048.0f);
+  const size_t base = ((((size_t)ct * ns + sk) * 2 + qq) * 2) * 2;  // [ct][s][q][part][h]
+  dst[((base + 0 + hh) * 64 + col) * 8 + j] = (_Float16)sc;
+  dst[((base + 2 + hh) * 64 + col) * 8 + j] = lo;
+}
+
 __global__ void scale_kernel(float* __restrict__ x, int64_t n, float s) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = x[i] * s;
@@ -1222,9 +1258,15 @@ int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, 
 
 int ifd_tr_pack_conv_x3(const float* w, int cout, int cin, int taps, int cin_pad16, int cout_pad, int transpose,
                         void* wx3, unsigned* guard, void* stream) {
-  if (!w || !wx3 || !guard || taps != 9 || cin_pad16 % 16 || cout_pad % 64) {
+  if (!w || !wx3 || !guard || (taps != 9 && taps != 1) || cin_pad16 % (taps == 1 ? 32 : 16) || cout_pad % 64) {
     set_error("ifd_tr_pack_conv_x3: bad arguments");
     return 2;
+  }
+  if (taps == 1) {
+    const int64_t tot = (int64_t)(cout_pad / 64) * (cin_pad16 / 32) * 2 * 2 * 64 * 8;
+    hipLaunchKernelGGL(pack_conv1x1_x3_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, w, cout, cin,
+                       cin_pad16, cout_pad, transpose, (_Float16*)wx3, guard);
+    return TR_LAST();
   }
   const int64_t tot = (int64_t)(cout_pad / 64) * (cin_pad16 / 16) * 9 * 2 * 64 * 8;
   hipLaunchKernelGGL(pack_conv_x3_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, w, cout, cin, cin_pad16,
@@ -1232,32 +1274,58 @@ int ifd_tr_pack_conv_x3(const float* w, int cout, int cin, int taps, int cin_pad
   return TR_LAST();
 }
 
+// taps = 1: the split kernel's 1x1-only launch (the operand as 32-channel skip chunks, no main
+// segment); a residual then goes through the split-K reduction (ksplit >= 2), as unet.hip does
 static void conv_x3_params(ConvParams& p, const float* x0, int c0, const float* x1, int c1, int N, int H,
-                           const void* wx3, const float* bias, int cin_pad, int cout, const float* res, float* out) {
+                           const void* wx3, const float* bias, int cin_pad, int cout, const float* res, float* out,
+                           int taps = 9) {
   conv_params(p, x0, c0, x1, c1, N, H, (const float*)wx3, bias, cin_pad, cout, cout, 64, 9, res, out);
   p.opt_bm128 = 0;
   p.x3_nprod = 3;
+  if (taps == 1) {
+    p.s0 = x0; p.sc0 = c0; p.s1 = nullptr; p.sc1 = 0;
+    p.wskip = (const float*)wx3; p.cs_pad = cin_pad;
+    p.in0 = nullptr; p.c0 = 0; p.in1 = nullptr; p.c1 = 0; p.cin_pad = 0;
+    conv_geometry(p, H, H, N, 64, cin_pad / 32, true);
+    if (res && p.ksplit == 1 && (cin_pad / 32) % 2 == 0) p.ksplit = 2;
+    return;
+  }
   conv_geometry(p, H, H, N, 64, cin_pad / 16, true);
 }
 
 int64_t ifd_tr_conv_x3_part_floats(int N, int H, int cin_pad, int cout) {
   ConvParams p;
   conv_x3_params(p, nullptr, cin_pad, nullptr, 0, N, H, nullptr, nullptr, cin_pad, cout, nullptr, nullptr);
-  return p.ksplit > 1 ? (int64_t)p.ksplit * N * H * H * cout : 0;
+  ConvParams q;  // the 1x1 geometry with a residual (the larger of the two)
+  conv_x3_params(q, nullptr, cin_pad, nullptr, 0, N, H, nullptr, nullptr, cin_pad, cout, (const float*)1, nullptr, 1);
+  const int S = p.ksplit > q.ksplit ? p.ksplit : q.ksplit;
+  return S > 1 ? (int64_t)S * N * H * H * cout : 0;
 }
 
 int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3, const float* bias,
                    int cin_pad, int cout, const float* res, float* out, float* part, int64_t part_floats,
                    unsigned* guard, void* stream) {
+  return ifd_tr_conv_x3_taps(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, 9,
+                             stream);
+}
+
+int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
+                        const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
+                        int64_t part_floats, unsigned* guard, int wx3_taps, void* stream) {
   if ((H & (H - 1)) || c0 + c1 != cin_pad || !x0 || !out || !wx3 || !bias || !guard) {
     set_error("ifd_tr_conv_x3: unsupported arguments");
     return 2;
   }
   ConvParams p;
-  conv_x3_params(p, x0, c0, c1 ? x1 : nullptr, c1, N, H, wx3, bias, cin_pad, cout, res, out);
+  const int taps = wx3_taps;
+  if (taps == 1 && (c1 || cin_pad % 32)) {
+    set_error("ifd_tr_conv_x3: 1x1 needs one input with cin % 32 == 0");
+    return 3;
+  }
+  conv_x3_params(p, x0, c0, c1 ? x1 : nullptr, c1, N, H, wx3, bias, cin_pad, cout, res, out, taps);
   p.guard = guard;
   const int nct = cout / 64;  // the non-SKIP split kernel decodes channel tiles by shifts
-  if (cout % 64 || (nct & (nct - 1)) || !conv_x3_eligible(p, 9, XF_NONE, 64)) {
+  if (cout % 64 || (taps == 9 && (nct & (nct - 1))) || !conv_x3_eligible(p, taps, XF_NONE, 64)) {
     set_error("ifd_tr_conv_x3: shape not eligible for the split kernel (use ifd_tr_conv)");
     return 3;
   }

@@ -37,6 +37,7 @@ TRAIN_EXPORTS = {
     "ifd_tr_pack_conv_x3": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "ifd_tr_conv_x3_part_floats": (i64, [i32, i32, i32, i32]),
     "ifd_tr_conv_x3": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, vp]),
+    "ifd_tr_conv_x3_taps": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
@@ -194,27 +195,30 @@ class UNetTrainer:
     def _conv_x3(self, x, cin_x, N, H, name, bias_name, res, x1, c1, transpose):
         """The conv on the 3xf16 split kernel, or None when its shape is not eligible (fp32 kernel then)."""
         w = self.p(name)
-        if w.dim() != 4 or w.shape[2] * w.shape[3] != 9:
+        taps = int(np.prod(w.shape[2:])) if w.dim() > 2 else 1
+        if taps not in (1, 9):
             return None
         cout, cin = w.shape[0], w.shape[1]
         pout, pin = (cout, cin) if not transpose else (cin, cout)
         nct = pout // 64
-        if pout % 64 or nct & (nct - 1) or cin_x + c1 != _pad(pin, 16) or cin_x % 16 or c1 % 16:
+        if taps == 9 and (pout % 64 or nct & (nct - 1) or cin_x + c1 != _pad(pin, 16) or cin_x % 16 or c1 % 16):
+            return None
+        if taps == 1 and (pout % 64 or c1 or cin_x != pin or cin_x % 32):
             return None
         cin_pad = cin_x + c1
         key = (name, int(transpose), "x3")
         wx3 = self._pack_cache.get(key)
         if wx3 is None:
-            wx3 = self._empty(pout * cin_pad * 9)
-            chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, 9, cin_pad, pout, int(transpose), P(wx3), P(self._guard),
-                                          self.s))
+            wx3 = self._empty(pout * cin_pad * taps)
+            chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, taps, cin_pad, pout, int(transpose), P(wx3),
+                                          P(self._guard), self.s))
             self._pack_cache[key] = wx3
         b = self.p(bias_name) if bias_name else self._zero_bias
         out = self._empty(N, H, H, pout)
         pf = lib().ifd_tr_conv_x3_part_floats(N, H, cin_pad, pout)
         part = self._empty(max(pf, 1))
-        rc = lib().ifd_tr_conv_x3(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, pout, P(res), P(out), P(part), pf,
-                                  P(self._guard), self.s)
+        rc = lib().ifd_tr_conv_x3_taps(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, pout, P(res), P(out),
+                                       P(part), pf, P(self._guard), taps, self.s)
         if rc == 3:
             return None
         chk(rc)

@@ -35,7 +35,8 @@ int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, 
                 int64_t part_floats, void* stream);
 /* 3xf16 training convs (the sampler's split kernel, conv_x3.hip, on a materialised input: no prologue).
  * ifd_tr_pack_conv_x3: W[cout][cin][9] (transpose=1: the dgrad conv, taps flipped) -> the split packing
- * [cout_pad/64][cin_pad16/16][9][part][h][64][8] f16 (wx3: cout_pad * cin_pad16 * 9 floats); sets bit 2 of
+ * [cout_pad/64][cin_pad16/16][9][part][h][64][8] f16 (wx3: cout_pad * cin_pad16 * 9 floats); taps = 1: the
+ * 1x1 chunk packing [cout_pad/64][cin/32][2][part][h][64][8] (cout_pad * cin floats); sets bit 2 of
  * *guard when a weight is outside the split's range (|w| >= 32).
  * ifd_tr_conv_x3: the same contract as ifd_tr_conv for 3x3 convs with cout % 64 == 0, cin % 16 == 0 and
  * maps of >= 16x16 (8x8: N % 4 == 0); returns 3 (nothing launched) for any other shape, so the caller runs
@@ -46,6 +47,11 @@ int64_t ifd_tr_conv_x3_part_floats(int N, int H, int cin_pad, int cout);
 int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3, const float* bias,
                    int cin_pad, int cout, const float* res, float* out, float* part, int64_t part_floats,
                    unsigned* guard, void* stream);
+/* ifd_tr_conv_x3 for 3x3 (taps 9) or 1x1 (taps 1: cin % 32 == 0, weights packed by ifd_tr_pack_conv_x3 with
+ * taps 1, part size from ifd_tr_conv_x3_part_floats). */
+int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
+                        const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
+                        int64_t part_floats, unsigned* guard, int taps, void* stream);
 /* x[i] *= s (the loss scale of the 3xf16 backward and its removal from the gradients). */
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream);
 /* dw[cout][c0+c1][taps] += sum_pixels dy (x) shifted concat(x0, x1); db[cout] += column sums of dy. */
