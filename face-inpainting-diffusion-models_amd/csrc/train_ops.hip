@@ -616,19 +616,29 @@ __global__ void gn_stat_final_kernel(const double* __restrict__ part, int nsl, i
 
 __device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + expf(-z)); }
 
+// 4 consecutive channels per thread (C % 32 == 0): one 16-B load / store and two 64-bit divisions per
+// 4 elements instead of per element (the per-element int64 div/mod made these passes VALU-bound)
 __global__ void gn_apply_kernel(const float* __restrict__ x, int64_t tot, int HW, int C, const float* __restrict__ stats,
                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                 const float* __restrict__ ss, int ss_stride, int act_silu, float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
   if (i >= tot) return;
-  const int c = (int)(i % C);
   const int64_t pix = i / C;
+  const int c0 = (int)(i - pix * C);
   const int n = (int)(pix / HW);
-  const int g = c / (C / 32);
-  const float mean = stats[(n * 32 + g) * 2], rstd = stats[(n * 32 + g) * 2 + 1];
-  float z = (x[i] - mean) * rstd * gamma[c] + beta[c];
-  if (ss) z = z * (1.0f + ss[(int64_t)n * ss_stride + c]) + ss[(int64_t)n * ss_stride + C + c];
-  out[i] = act_silu ? z * sigm(z) : z;
+  const int cpg = C / 32;
+  const f32x4 xv = *reinterpret_cast<const f32x4*>(x + i);
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = c0 + j;
+    const int g = c / cpg;
+    const float mean = stats[(n * 32 + g) * 2], rstd = stats[(n * 32 + g) * 2 + 1];
+    float z = (xv[j] - mean) * rstd * gamma[c] + beta[c];
+    if (ss) z = z * (1.0f + ss[(int64_t)n * ss_stride + c]) + ss[(int64_t)n * ss_stride + C + c];
+    o[j] = act_silu ? z * sigm(z) : z;
+  }
+  *reinterpret_cast<f32x4*>(out + i) = o;
 }
 
 // GroupNorm(+ scale/shift)(+ SiLU) backward. With xhat = (x - mean) rstd, nrm = xhat gamma + beta,
@@ -730,18 +740,29 @@ __global__ void gn_bwd_param_kernel(GnBwdArgs a, const float* __restrict__ nc, f
   dbeta[c] += (float)b;
 }
 __global__ void gn_bwd_dx_kernel(GnBwdArgs a, const float* __restrict__ red, float* __restrict__ dx, int accumulate) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);  // 4 channels per thread
   const int64_t tot = (int64_t)a.N * a.HW * a.C;
   if (i >= tot) return;
-  const int c = (int)(i % a.C);
-  const int n = (int)(i / ((int64_t)a.HW * a.C));
-  float xhat, nrm, dz, onep;
-  gn_bwd_point(a, n, c, a.x[i], a.dout[i], xhat, nrm, dz, onep);
-  const int g = c / (a.C / 32);
-  const float rstd = a.stats[(n * 32 + g) * 2 + 1];
-  const float dxhat = dz * onep * a.gamma[c];
-  const float v = rstd * (dxhat - red[(n * 32 + g) * 2] - xhat * red[(n * 32 + g) * 2 + 1]);
-  dx[i] = accumulate ? dx[i] + v : v;
+  const int64_t pix = i / a.C;
+  const int c0 = (int)(i - pix * a.C);
+  const int n = (int)(pix / a.HW);
+  const f32x4 xv = *reinterpret_cast<const f32x4*>(a.x + i);
+  const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dout + i);
+  f32x4 prev = {0.f, 0.f, 0.f, 0.f};
+  if (accumulate) prev = *reinterpret_cast<const f32x4*>(dx + i);
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = c0 + j;
+    float xhat, nrm, dz, onep;
+    gn_bwd_point(a, n, c, xv[j], dv[j], xhat, nrm, dz, onep);
+    const int g = c / (a.C / 32);
+    const float rstd = a.stats[(n * 32 + g) * 2 + 1];
+    const float dxhat = dz * onep * a.gamma[c];
+    const float v = rstd * (dxhat - red[(n * 32 + g) * 2] - xhat * red[(n * 32 + g) * 2 + 1]);
+    o[j] = accumulate ? prev[j] + v : v;
+  }
+  *reinterpret_cast<f32x4*>(dx + i) = o;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -768,6 +789,67 @@ __global__ void resample_kernel(const float* __restrict__ x, int N, int Hin, int
     s = s + x[b0 + rs + C];
     out[i] = s / 4.0f;
   }
+}
+// 4 channels per thread (C % 4 == 0): one index decode per 4 values
+__global__ void resample4_kernel(const float* __restrict__ x, int N, int Hin, int C, int mode, float* __restrict__ out) {
+  const int Ho = mode == 1 ? 2 * Hin : Hin / 2;
+  const int64_t tot = (int64_t)N * Ho * Ho * C;
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= tot) return;
+  int64_t r = i / C;
+  const int c = (int)(i - r * C);
+  const int64_t r2 = r / Ho;
+  const int xo = (int)(r - r2 * Ho);
+  const int n = (int)(r2 / Ho);
+  const int yo = (int)(r2 - (int64_t)n * Ho);
+  if (mode == 1) {
+    *reinterpret_cast<f32x4*>(out + i) =
+        *reinterpret_cast<const f32x4*>(x + (((int64_t)n * Hin + yo / 2) * Hin + xo / 2) * C + c);
+  } else {
+    const int64_t b0 = (((int64_t)n * Hin + 2 * yo) * Hin + 2 * xo) * C + c;
+    const int64_t rs = (int64_t)Hin * C;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(x + b0), a1 = *reinterpret_cast<const f32x4*>(x + b0 + C);
+    const f32x4 a2 = *reinterpret_cast<const f32x4*>(x + b0 + rs), a3 = *reinterpret_cast<const f32x4*>(x + b0 + rs + C);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = a0[j];
+      v = v + a1[j];
+      v = v + a2[j];
+      v = v + a3[j];
+      o[j] = v / 4.0f;
+    }
+    *reinterpret_cast<f32x4*>(out + i) = o;
+  }
+}
+__global__ void resample4_bwd_kernel(const float* __restrict__ dy, int N, int Hin, int C, int mode,
+                                     float* __restrict__ dx, int accumulate) {
+  const int64_t tot = (int64_t)N * Hin * Hin * C;
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= tot) return;
+  int64_t r = i / C;
+  const int c = (int)(i - r * C);
+  const int64_t r2 = r / Hin;
+  const int x = (int)(r - r2 * Hin);
+  const int n = (int)(r2 / Hin);
+  const int y = (int)(r2 - (int64_t)n * Hin);
+  f32x4 v;
+  if (mode == 1) {
+    const int Ho = 2 * Hin;
+    const int64_t b0 = (((int64_t)n * Ho + 2 * y) * Ho + 2 * x) * C + c;
+    const int64_t rs = (int64_t)Ho * C;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(dy + b0), a1 = *reinterpret_cast<const f32x4*>(dy + b0 + C);
+    const f32x4 a2 = *reinterpret_cast<const f32x4*>(dy + b0 + rs), a3 = *reinterpret_cast<const f32x4*>(dy + b0 + rs + C);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ((a0[j] + a1[j]) + a2[j]) + a3[j];
+  } else {
+    const int Ho = Hin / 2;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(dy + (((int64_t)n * Ho + y / 2) * Ho + x / 2) * C + c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = a[j] / 4.0f;
+  }
+  if (accumulate) v = *reinterpret_cast<const f32x4*>(dx + i) + v;
+  *reinterpret_cast<f32x4*>(dx + i) = v;
 }
 // dx at the input resolution from dy at the output resolution
 __global__ void resample_bwd_kernel(const float* __restrict__ dy, int N, int Hin, int C, int mode,
@@ -798,15 +880,30 @@ __global__ void add_kernel(const float* __restrict__ a, const float* __restrict_
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = a[i] + b[i];
 }
+__global__ void add4_kernel(const float* __restrict__ a, const float* __restrict__ b, float* out, int64_t n) {
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) *reinterpret_cast<f32x4*>(out + i) = *reinterpret_cast<const f32x4*>(a + i) + *reinterpret_cast<const f32x4*>(b + i);
+}
 // dst[p][doff + c] (+)= src[p][soff + c], c < nc: concat assembly and the split of its gradient
 __global__ void copy_channels_kernel(const float* __restrict__ src, int cs, int soff, float* __restrict__ dst, int cd,
                                      int doff, int nc, int64_t npix, int accumulate) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= npix * nc) return;
   const int64_t p = i / nc;
-  const int c = (int)(i % nc);
+  const int c = (int)(i - p * nc);
   const float v = src[p * cs + soff + c];
   float* d = dst + p * cd + doff + c;
+  *d = accumulate ? *d + v : v;
+}
+// the same, 4 channels per thread (every count and offset a multiple of 4)
+__global__ void copy_channels4_kernel(const float* __restrict__ src, int cs, int soff, float* __restrict__ dst, int cd,
+                                      int doff, int nc, int64_t npix, int accumulate) {
+  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= npix * nc) return;
+  const int64_t p = i / nc;
+  const int c = (int)(i - p * nc);
+  const f32x4 v = *reinterpret_cast<const f32x4*>(src + p * cs + soff + c);
+  f32x4* d = reinterpret_cast<f32x4*>(dst + p * cd + doff + c);
   *d = accumulate ? *d + v : v;
 }
 
@@ -1466,7 +1563,7 @@ int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, cons
   hipLaunchKernelGGL(gn_stat_partial_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, work);
   hipLaunchKernelGGL(gn_stat_final_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, work, nsl, HW, C, N, stats);
   const int64_t tot = (int64_t)N * HW * C;
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid1(tot)), dim3(TB), 0, s, x, tot, HW, C, stats, gamma, beta, ss,
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid1(tot / 4)), dim3(TB), 0, s, x, tot, HW, C, stats, gamma, beta, ss,
                      ss_stride, act_silu, out);
   return TR_LAST();
 }
@@ -1490,7 +1587,7 @@ int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const
   hipLaunchKernelGGL(gn_bwd_group_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, a, nc, red);
   hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
   const int64_t tot = (int64_t)N * HW * C;
-  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(grid1(tot)), dim3(TB), 0, s, a, red, dx, accumulate);
+  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(grid1(tot / 4)), dim3(TB), 0, s, a, red, dx, accumulate);
   return TR_LAST();
 }
 
@@ -1498,28 +1595,44 @@ int ifd_tr_resample(const float* x, int N, int Hin, int C, int mode, float* out,
   if (mode != 1 && mode != 2) { set_error("ifd_tr_resample: mode 1 (up) or 2 (down)"); return 2; }
   const int Ho = mode == 1 ? 2 * Hin : Hin / 2;
   const int64_t tot = (int64_t)N * Ho * Ho * C;
-  hipLaunchKernelGGL(resample_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, x, N, Hin, C, mode, out);
+  if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0)
+    hipLaunchKernelGGL(resample4_kernel, dim3(grid1(tot / 4)), dim3(TB), 0, (hipStream_t)stream, x, N, Hin, C, mode, out);
+  else
+    hipLaunchKernelGGL(resample_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, x, N, Hin, C, mode, out);
   return TR_LAST();
 }
 
 int ifd_tr_resample_bwd(const float* dy, int N, int Hin, int C, int mode, float* dx, int accumulate, void* stream) {
   if (mode != 1 && mode != 2) { set_error("ifd_tr_resample_bwd: mode 1 (up) or 2 (down)"); return 2; }
   const int64_t tot = (int64_t)N * Hin * Hin * C;
-  hipLaunchKernelGGL(resample_bwd_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, dy, N, Hin, C, mode, dx,
-                     accumulate);
+  if (C % 4 == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)dx & 15) == 0)
+    hipLaunchKernelGGL(resample4_bwd_kernel, dim3(grid1(tot / 4)), dim3(TB), 0, (hipStream_t)stream, dy, N, Hin, C,
+                       mode, dx, accumulate);
+  else
+    hipLaunchKernelGGL(resample_bwd_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, dy, N, Hin, C, mode,
+                       dx, accumulate);
   return TR_LAST();
 }
 
 int ifd_tr_add(const float* a, const float* b, float* out, int64_t n, void* stream) {
-  hipLaunchKernelGGL(add_kernel, dim3(grid1(n)), dim3(TB), 0, (hipStream_t)stream, a, b, out, n);
+  if (n % 4 == 0 && (((uintptr_t)a | (uintptr_t)b | (uintptr_t)out) & 15) == 0)
+    hipLaunchKernelGGL(add4_kernel, dim3(grid1(n / 4)), dim3(TB), 0, (hipStream_t)stream, a, b, out, n);
+  else
+    hipLaunchKernelGGL(add_kernel, dim3(grid1(n)), dim3(TB), 0, (hipStream_t)stream, a, b, out, n);
   return TR_LAST();
 }
 
 int ifd_tr_copy_channels(const float* src, int cs, int soff, float* dst, int cd, int doff, int nc, int64_t npix,
                          int accumulate, void* stream) {
   if (soff + nc > cs || doff + nc > cd) { set_error("ifd_tr_copy_channels: channel range"); return 2; }
-  hipLaunchKernelGGL(copy_channels_kernel, dim3(grid1(npix * nc)), dim3(TB), 0, (hipStream_t)stream, src, cs, soff, dst,
-                     cd, doff, nc, npix, accumulate);
+  const bool v4 = cs % 4 == 0 && soff % 4 == 0 && cd % 4 == 0 && doff % 4 == 0 && nc % 4 == 0 &&
+                  ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0;
+  if (v4)
+    hipLaunchKernelGGL(copy_channels4_kernel, dim3(grid1(npix * nc / 4)), dim3(TB), 0, (hipStream_t)stream, src, cs,
+                       soff, dst, cd, doff, nc, npix, accumulate);
+  else
+    hipLaunchKernelGGL(copy_channels_kernel, dim3(grid1(npix * nc)), dim3(TB), 0, (hipStream_t)stream, src, cs, soff,
+                       dst, cd, doff, nc, npix, accumulate);
   return TR_LAST();
 }
 

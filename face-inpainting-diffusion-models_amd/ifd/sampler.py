@@ -184,10 +184,12 @@ class InpaintingSampler:
         L = _lib.lib()
         h = self.model.handle(torch.device(device)) if fused else None
         keep = None if fused else 1 - mk
+        # every step's timestep vector in one host-to-device copy (rows are contiguous views)
+        t_tab = torch.as_tensor(np.repeat(np.asarray(seq, dtype=np.int64)[:, None], B, 1)).to(device)
         for k, tau in it:
             tau = int(tau)
             c = ddim_coeffs(self.diffusion.alphas_cumprod, seq, k, eta, clip_denoised)
-            t = torch.full((B,), tau, device=device, dtype=torch.int64)
+            t = t_tab[k]
             with torch.no_grad():
                 out = None if fused else model_fn(img, t, gt=gt, gt_keep_mask=keep)
                 noise = self._randn(shape, device) if c.use_noise else None
@@ -227,9 +229,11 @@ class InpaintingSampler:
         L = _lib.lib()
         h = self.model.handle(torch.device(device)) if fused else None
         keep = None if fused else 1 - mk
+        T = self.diffusion.num_timesteps
+        t_tab = torch.as_tensor(np.repeat(np.arange(T, dtype=np.int64)[:, None], B, 1)).to(device)
         for i in indices:
             c = ddpm_coeffs(self.diffusion, i, clip_denoised)
-            t = torch.full((B,), i, device=device, dtype=torch.int64)
+            t = t_tab[i]
             with torch.no_grad():
                 out = None if fused else model_fn(img, t, gt=gt, gt_keep_mask=keep)
                 noise = self._randn(shape, device)
