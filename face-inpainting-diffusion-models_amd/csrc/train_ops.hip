@@ -416,43 +416,35 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
                    : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     };
-    auto store = [&](_Float16* L) {
-      if (do_cs)
+    // staging of one chunk in WX_PARTS slices (items: the WX_DI dY quads, then the WX_XI halo quads), so
+    // that chunk c + 1's split and LDS writes run between chunk c's k-steps
+    constexpr int WX_ITEMS = WX_DI + WX_XI, WX_PARTS = WX_PX / 16, WX_PER = (WX_ITEMS + WX_PARTS - 1) / WX_PARTS;
+    auto store_part = [&](_Float16* L, int part) {
+      _Float16* X = L + WX_D;
 #pragma unroll
-        for (int k = 0; k < WX_DI; ++k) csum += dv[k];
-#pragma unroll
-      for (int k = 0; k < WX_DI; ++k) {
-        const int m = (tid + 256 * k) >> 4;
+      for (int it = 0; it < WX_ITEMS; ++it) {
+        if (it / WX_PER != part) continue;
+        const bool isd = it < WX_DI;
+        const int k = isd ? it : it - WX_DI;
+        const f32x4 v = isd ? dv[k] : xv[k];
+        const int row = isd ? (tid + 256 * k) >> 4 : (tid + 256 * k) >> 4;
+        if (!isd && row >= HP) continue;
+        if (isd && do_cs) csum += v;
         wx_h4 hi, lo;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float x = dv[k][j];
+          float x = v[j];
           asm volatile("" : "+v"(x));
           const _Float16 hh = (_Float16)x;
           hi[j] = hh;
           lo[j] = (_Float16)(x - (float)hh);
           gmax = fmaxf(gmax, fabsf(x));
         }
-        const int o = wx_off(m, 4 * cq);
-        *(wx_lds_u2*)(L + o) = __builtin_bit_cast(wx_u2, hi);
-        *(wx_lds_u2*)(L + WX_PX * 64 + o) = __builtin_bit_cast(wx_u2, lo);
-      }
-      _Float16* X = L + WX_D;
-#pragma unroll
-      for (int k = 0; k < WX_XI; ++k) {
-        const int hp = (tid + 256 * k) >> 4;
-        if (hp < HP) {
-          wx_h4 hi, lo;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float x = xv[k][j];
-            asm volatile("" : "+v"(x));
-            const _Float16 hh = (_Float16)x;
-            hi[j] = hh;
-            lo[j] = (_Float16)(x - (float)hh);
-            gmax = fmaxf(gmax, fabsf(x));
-          }
-          const int o = wx_off(hp, 4 * cq);
+        const int o = wx_off(row, 4 * cq);
+        if (isd) {
+          *(wx_lds_u2*)(L + o) = __builtin_bit_cast(wx_u2, hi);
+          *(wx_lds_u2*)(L + WX_PX * 64 + o) = __builtin_bit_cast(wx_u2, lo);
+        } else {
           *(wx_lds_u2*)(X + o) = __builtin_bit_cast(wx_u2, hi);
           *(wx_lds_u2*)(X + WX_HMAX * 64 + o) = __builtin_bit_cast(wx_u2, lo);
         }
@@ -462,36 +454,81 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
     // which 8 of the k-step's 16 pixels); lane 4q + p of the group addresses row q, columns 4p .. 4p + 3
     const int G = lane >> 4, q = (lane & 15) >> 2, pcol = 4 * (lane & 3);
     const int cA = wr + 16 * (G & 1) + pcol, cB = wc + 16 * (G & 1) + pcol;
+    // prologue: chunk c_beg staged, chunk c_beg + 1 in flight. Iteration c: MFMAs of chunk c from
+    // lds[c & 1] with chunk c + 1's staging slices between its k-steps into lds[(c + 1) & 1] (read by
+    // chunk c - 1, whose MFMAs every wave finished before the previous barrier), then chunk c + 2's loads
     load(c_beg);
+#pragma unroll
+    for (int part = 0; part < WX_PARTS; ++part) store_part(lds[c_beg & 1], part);
+    __syncthreads();
+    if (c_beg + 1 < c_end) load(c_beg + 1);
     for (int64_t c = c_beg; c < c_end; ++c) {
       _Float16* L = lds[c & 1];
-      store(L);
-      __syncthreads();
-      if (c + 1 < c_end) load(c + 1);
+      _Float16* Ln = lds[(c + 1) & 1];
+      const bool nxt = c + 1 < c_end;
       const _Float16* Dh = L;
       const _Float16* Dl = L + WX_PX * 64;
       const _Float16* Xh = L + WX_D;
       const _Float16* Xl = Xh + WX_HMAX * 64;
-#pragma unroll
-      for (int st = 0; st < WX_PX / 16; ++st) {
-        const int m0 = 16 * st + 8 * h;  // this lane-half's 8 pixels of the k-step: one row segment
+      // Software-pipelined: taps in pairs whose MFMAs alternate (no back-to-back accumulator
+      // dependence), the next pair's B fragments read after the current pair's first MFMAs, the
+      // next k-step's A fragments during the last pair (a read the MFMA waits on costs its latency).
+      auto fetchA = [&](int st, wx_h8& ahi, wx_h8& alo) {
+        const int m0 = 16 * st + 8 * h;
         const int oa0 = wx_off(m0 + q, cA), oa1 = wx_off(m0 + 4 + q, cA);
         const wx_h4 ah0 = wx_tr(Dh, oa0), ah1 = wx_tr(Dh, oa1), al0 = wx_tr(Dl, oa0), al1 = wx_tr(Dl, oa1);
-        const wx_h8 ahi = {ah0[0], ah0[1], ah0[2], ah0[3], ah1[0], ah1[1], ah1[2], ah1[3]};
-        const wx_h8 alo = {al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
+        ahi = wx_h8{ah0[0], ah0[1], ah0[2], ah0[3], ah1[0], ah1[1], ah1[2], ah1[3]};
+        alo = wx_h8{al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
+      };
+      auto fetchB = [&](int st, int t, wx_h8& bhi, wx_h8& blo) {
+        const int m0 = 16 * st + 8 * h;  // this lane-half's 8 pixels of the k-step: one row segment
         const int hb = (m0 >> lwc) * HWc + (m0 & (Wc - 1));
+        const int r0 = TAPS == 9 ? hb + (t / 3) * HWc + (t % 3) : hb;
+        const int ob0 = wx_off(r0 + q, cB), ob1 = wx_off(r0 + 4 + q, cB);
+        const wx_h4 bh0 = wx_tr(Xh, ob0), bh1 = wx_tr(Xh, ob1), bl0 = wx_tr(Xl, ob0), bl1 = wx_tr(Xl, ob1);
+        bhi = wx_h8{bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
+        blo = wx_h8{bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
+      };
+      constexpr int NST = WX_PX / 16, NPAIR = (TAPS + 1) / 2;
+      wx_h8 ahi, alo, b0h, b0l, b1h, b1l;
+      fetchA(0, ahi, alo);
+      fetchB(0, 0, b0h, b0l);
+      if (TAPS > 1) fetchB(0, 1, b1h, b1l);
 #pragma unroll
-        for (int t = 0; t < TAPS; ++t) {
-          const int r0 = TAPS == 9 ? hb + (t / 3) * HWc + (t % 3) : hb;
-          const int ob0 = wx_off(r0 + q, cB), ob1 = wx_off(r0 + 4 + q, cB);
-          const wx_h4 bh0 = wx_tr(Xh, ob0), bh1 = wx_tr(Xh, ob1), bl0 = wx_tr(Xl, ob0), bl1 = wx_tr(Xl, ob1);
-          const wx_h8 bhi = {bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
-          const wx_h8 blo = {bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, bhi, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, blo, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, bhi, acc[t], 0, 0, 0);
+      for (int st = 0; st < NST; ++st) {
+#pragma unroll
+        for (int pp = 0; pp < NPAIR; ++pp) {
+          const int t0 = 2 * pp, t1 = 2 * pp + 1;
+          const bool two = t1 < TAPS;
+          acc[t0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b0h, acc[t0], 0, 0, 0);
+          if (two) acc[t1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b1h, acc[t1], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          // next pair (or the next k-step's first pair, and its A fragments)
+          wx_h8 n0h, n0l, n1h, n1l, nah, nal;
+          const bool last = pp + 1 == NPAIR;
+          const int nst = last ? st + 1 : st, nt0 = last ? 0 : t0 + 2;
+          const bool more = nst < NST;
+          if (more) {
+            fetchB(nst, nt0, n0h, n0l);
+            if (nt0 + 1 < TAPS) fetchB(nst, nt0 + 1, n1h, n1l);
+            if (last) fetchA(nst, nah, nal);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          acc[t0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b0l, acc[t0], 0, 0, 0);
+          if (two) acc[t1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b1l, acc[t1], 0, 0, 0);
+          acc[t0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b0h, acc[t0], 0, 0, 0);
+          if (two) acc[t1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b1h, acc[t1], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (more) {
+            b0h = n0h; b0l = n0l;
+            if (nt0 + 1 < TAPS) { b1h = n1h; b1l = n1l; }
+            if (last) { ahi = nah; alo = nal; }
+          }
         }
+        if (nxt) store_part(Ln, st);  // (block-uniform)
+        __builtin_amdgcn_sched_barrier(0);
       }
+      if (c + 2 < c_end) load(c + 2);
       __syncthreads();
     }
   }
@@ -1508,8 +1545,9 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
 int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                          int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
                          int64_t colpart_floats, unsigned* guard, void* stream) {
-  // the split kernel: 3x3 or 1x1, one input tensor, power-of-two maps >= 8; else fp32
-  if ((taps != 9 && taps != 1) || c1 || H < 8 || (H & (H - 1)) || !guard)
+  // the split kernel: 3x3 or 1x1, one input tensor, power-of-two maps >= 8, channel counts in 16-B quads
+  // (its staging loads four channels at a time); else fp32
+  if ((taps != 9 && taps != 1) || c1 || H < 8 || (H & (H - 1)) || !guard || cout % 4 || c0 % 4)
     return ifd_tr_conv_wgrad(dy, cout, x0, c0, x1, c1, N, H, taps, dw, db, part, part_floats, colpart, colpart_floats,
                              stream);
   const int64_t P = (int64_t)N * H * H;
