@@ -71,9 +71,10 @@ int ifd_load_weights(ifd_handle* h, const char* name, const float* data, const i
 int ifd_finalize(ifd_handle* h);
 /* Conv arithmetic of the handle (default IFD_PREC_FP32):
  *   IFD_PREC_FP32   every conv on v_mfma_f32_32x32x2_f32: an exact fp32 fma chain.
- *   IFD_PREC_3XF16  layers with a split kernel run each fp32 operand as two f16 parts (hi + 2^-11 lo)
- *                   and three f16 MFMAs into one fp32 accumulator: fp32-level error,
- *                   5.3x the fp32 MFMA rate; the other layers stay fp32. Takes effect on the next call.
+ *   IFD_PREC_3XF16  layers with a split kernel (every 3x3 conv, the 1x1 convs, the output head) run
+ *                   each fp32 operand as two f16 parts (hi + 2^-11 lo) and three f16 MFMAs into one
+ *                   fp32 accumulator: fp32-level error, 5.3x the fp32 MFMA rate; the
+ *                   other layers stay fp32. Takes effect on the next call.
  * The reference has no such switch: its model runs in the caller's dtype (fp32 on this path). */
 #define IFD_PREC_FP32 0
 #define IFD_PREC_3XF16 1
@@ -101,7 +102,8 @@ int ifd_get_precision(ifd_handle* h, int* prec);
  *                          mode: N ranks x B/N images == one rank x B images). Slower on small layers.
  *   "conv_stream"     0..2 wide fp32 layers: one tile per workgroup / persistent 1 or 2 per CU
  *   "gn_fused"        0/1  GroupNorm statistics fused into the producing conv (1) or a separate pass
- *   "x3_off", "stream_cw", "conv_bm128", "lds_pad"   development switches (bisecting, tuning) */
+ *   "x3_off", "stream_cw", "conv_bm128", "lds_pad"   development switches (bisecting, tuning; x3_off
+ *                          bit 32 keeps the output head on the fp32 VALU kernel in the 3xf16 mode) */
 int ifd_set_option(ifd_handle* h, const char* key, int value);
 int ifd_get_option(ifd_handle* h, const char* key, int* value);
 /* Bytes of device workspace the handle holds (weights + activations). */
