@@ -201,7 +201,16 @@ class UNetTrainer:
         cout, cin = w.shape[0], w.shape[1]
         pout, pin = (cout, cin) if not transpose else (cin, cout)
         nct = pout // 64
-        if taps == 9 and (pout % 64 or nct & (nct - 1) or cin_x + c1 != _pad(pin, 16) or cin_x % 16 or c1 % 16):
+        # a 3x3 conv whose 64-channel tile count is not a power of two (the dgrad of the output blocks'
+        # concat convs: 384 = 6 x 64, 768 = 12 x 64 output channels) runs padded to the next power of two
+        # (zero weight rows) into a scratch tensor and is copied out: the split kernel decodes its
+        # channel tiles by shifts
+        ppad = pout
+        if taps == 9 and pout % 64 == 0 and nct & (nct - 1) and res is None and not bias_name:
+            ppad = 64 * (1 << (nct - 1).bit_length())
+        if taps == 9 and (pout % 64 or cin_x + c1 != _pad(pin, 16) or cin_x % 16 or c1 % 16):
+            return None
+        if taps == 9 and (ppad // 64) & (ppad // 64 - 1):
             return None
         if taps == 1 and (pout % 64 or c1 or cin_x != pin or cin_x % 32):
             return None
@@ -209,19 +218,23 @@ class UNetTrainer:
         key = (name, int(transpose), "x3")
         wx3 = self._pack_cache.get(key)
         if wx3 is None:
-            wx3 = self._empty(pout * cin_pad * taps)
-            chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, taps, cin_pad, pout, int(transpose), P(wx3),
+            wx3 = self._empty(ppad * cin_pad * taps)
+            chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, taps, cin_pad, ppad, int(transpose), P(wx3),
                                           P(self._guard), self.s))
             self._pack_cache[key] = wx3
         b = self.p(bias_name) if bias_name else self._zero_bias
-        out = self._empty(N, H, H, pout)
-        pf = lib().ifd_tr_conv_x3_part_floats(N, H, cin_pad, pout)
+        out = self._empty(N, H, H, ppad)
+        pf = lib().ifd_tr_conv_x3_part_floats(N, H, cin_pad, ppad)
         part = self._empty(max(pf, 1))
-        rc = lib().ifd_tr_conv_x3_taps(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, pout, P(res), P(out),
+        rc = lib().ifd_tr_conv_x3_taps(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, ppad, P(res), P(out),
                                        P(part), pf, P(self._guard), taps, self.s)
         if rc == 3:
             return None
         chk(rc)
+        if ppad != pout:
+            real = self._empty(N, H, H, pout)
+            self.copy_ch(out, ppad, 0, real, pout, 0, pout, N * H * H, False)
+            out = real
         return out
 
     def conv(self, x, cin_x, N, H, name, bias_name=None, res=None, x1=None, c1=0, transpose=False):
