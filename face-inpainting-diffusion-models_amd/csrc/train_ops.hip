@@ -605,17 +605,40 @@ __global__ void colsum_final_kernel(const float* __restrict__ part, int S, int C
 //   out = act((x - mean) * rstd * gamma + beta) [ * (1 + scale) + shift ]
 // ss (optional): [N][ss_stride], scale at [0, C), shift at [C, 2C) (the emb projection's chunk order).
 constexpr int GN_SL = 256;  // pixels per partial block
-__global__ void gn_stat_partial_kernel(const float* __restrict__ x, int HW, int C, double* __restrict__ part) {
-  // grid (slices, N); thread = channel (C <= 1024 in steps of blockDim)
-  __shared__ double s1[1024], s2[1024];
+// grid (slices, N), 256 threads. Thread = (row r, channel quad q): Q = C/4 quads side by side and
+// R = 256/Q rows striding the slice's pixels, so each 16-B load belongs to a wave that covers whole
+// pixel rows. Per-thread float64 sums are combined over the rows in LDS in a fixed order.
+__global__ __launch_bounds__(256) void gn_stat_partial_kernel(const float* __restrict__ x, int HW, int C,
+                                                              double* __restrict__ part) {
+  __shared__ double s1[1024], s2[1024];  // [row][C] (R * C <= 1024), then per channel in row 0
   const int n = blockIdx.y;
   const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, HW);
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  const int Q = C >> 2, R = 256 / Q;
+  const int q = threadIdx.x % Q, r = threadIdx.x / Q;
+  if (r < R) {
+    double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+    const float* xs = x + (int64_t)n * HW * C + 4 * q;
+    for (int p = p0 + r; p < p1; p += R) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xs + (int64_t)p * C);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double d = v[j];
+        a[j] += d;
+        b[j] += d * d;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[r * C + 4 * q + j] = a[j];
+      s2[r * C + 4 * q + j] = b[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {  // column c is read and written by thread c only
     double a = 0.0, b = 0.0;
-    for (int p = p0; p < p1; ++p) {
-      const double v = x[((int64_t)n * HW + p) * C + c];
-      a += v;
-      b += v * v;
+    for (int k = 0; k < R; ++k) {
+      a += s1[k * C + c];
+      b += s2[k * C + c];
     }
     s1[c] = a;
     s2[c] = b;
@@ -633,16 +656,22 @@ __global__ void gn_stat_partial_kernel(const float* __restrict__ x, int HW, int 
     o[1] = b;
   }
 }
-__global__ void gn_stat_final_kernel(const double* __restrict__ part, int nsl, int HW, int C, int N,
-                                     float* __restrict__ stats) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (n, g)
-  if (i >= N * 32) return;
+// one wave per (n, g): the lanes stride the slices, then a fixed butterfly (deterministic)
+__global__ __launch_bounds__(64) void gn_stat_final_kernel(const double* __restrict__ part, int nsl, int HW, int C,
+                                                           int N, float* __restrict__ stats) {
+  const int i = blockIdx.x;  // (n, g)
   const int n = i / 32, g = i % 32;
   double a = 0.0, b = 0.0;
-  for (int s = 0; s < nsl; ++s) {
+  for (int s = threadIdx.x; s < nsl; s += 64) {
     a += part[(((int64_t)n * nsl + s) * 32 + g) * 2];
     b += part[(((int64_t)n * nsl + s) * 32 + g) * 2 + 1];
   }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    b += __shfl_xor(b, off);
+  }
+  if (threadIdx.x) return;
   const double cnt = (double)HW * (C / 32);
   const double mean = a / cnt;
   double var = b / cnt - mean * mean;
@@ -708,24 +737,67 @@ __device__ __forceinline__ void gn_bwd_point(const GnBwdArgs& a, int n, int c, f
     dz = dav;
   }
 }
-__global__ void gn_bwd_partial_kernel(GnBwdArgs a, float* __restrict__ part) {
-  // grid (slices, N); part [N][nsl][C][3]
-  const int n = blockIdx.y;
+// grid (slices, N), 256 threads laid out as gn_stat_partial_kernel's (row, channel quad); a thread's
+// per-channel coefficients stay in registers and the per-point math is gn_bwd_point's
+__global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnBwdArgs a, float* __restrict__ part) {
+  // part [N][nsl][C][3]
+  __shared__ float red[3][1024];  // [row][C] (R * C <= 1024), then per channel in row 0
+  const int n = blockIdx.y, C = a.C;
   const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, a.HW);
-  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    for (int p = p0; p < p1; ++p) {
-      const int64_t i = ((int64_t)n * a.HW + p) * a.C + c;
-      float xhat, nrm, dz, onep;
-      gn_bwd_point(a, n, c, a.x[i], a.dout[i], xhat, nrm, dz, onep);
-      s1 += dz;
-      s2 += dz * nrm;
-      s3 += dz * onep * xhat;
+  const int Q = C >> 2, R = 256 / Q;
+  const int q = threadIdx.x % Q, r = threadIdx.x / Q;
+  if (r < R) {
+    const int c0 = 4 * q, cpg = C / 32;
+    float mean[4], rstd[4], gam[4], bet[4], onep[4], sh[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + j, g = c / cpg;
+      mean[j] = a.stats[(n * 32 + g) * 2];
+      rstd[j] = a.stats[(n * 32 + g) * 2 + 1];
+      gam[j] = a.gamma[c];
+      bet[j] = a.beta[c];
+      onep[j] = a.ss ? 1.0f + a.ss[(int64_t)n * a.ss_stride + c] : 1.0f;
+      sh[j] = a.ss ? a.ss[(int64_t)n * a.ss_stride + C + c] : 0.0f;
     }
-    float* o = part + (((int64_t)n * gridDim.x + blockIdx.x) * a.C + c) * 3;
-    o[0] = s1;
-    o[1] = s2;
-    o[2] = s3;
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, s3[4] = {0.f, 0.f, 0.f, 0.f};
+    const int64_t base = (int64_t)n * a.HW * C + c0;
+    for (int p = p0 + r; p < p1; p += R) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(a.x + base + (int64_t)p * C);
+      const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dout + base + (int64_t)p * C);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xhat = (xv[j] - mean[j]) * rstd[j];
+        const float nrm = xhat * gam[j] + bet[j];
+        const float z = a.ss ? nrm * onep[j] + sh[j] : nrm;
+        float dz = dv[j];
+        if (a.act_silu) {
+          const float sg = sigm(z);
+          dz = dv[j] * (sg * (1.0f + z * (1.0f - sg)));
+        }
+        s1[j] += dz;
+        s2[j] += dz * nrm;
+        s3[j] += dz * onep[j] * xhat;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[0][r * C + c0 + j] = s1[j];
+      red[1][r * C + c0 + j] = s2[j];
+      red[2][r * C + c0 + j] = s3[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float t1 = 0.f, t2 = 0.f, t3 = 0.f;
+    for (int k = 0; k < R; ++k) {
+      t1 += red[0][k * C + c];
+      t2 += red[1][k * C + c];
+      t3 += red[2][k * C + c];
+    }
+    float* o = part + (((int64_t)n * gridDim.x + blockIdx.x) * C + c) * 3;
+    o[0] = t1;
+    o[1] = t2;
+    o[2] = t3;
   }
 }
 // per (n, c): A1..A3 (float64 over slices) -> dss, and per-(n, g) means -> red[n][g][2]
@@ -735,6 +807,7 @@ __global__ void gn_bwd_reduce_kernel(GnBwdArgs a, const float* __restrict__ part
   if (i >= a.N * a.C) return;
   const int n = i / a.C, c = i % a.C;
   double s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll 8
   for (int s = 0; s < nsl; ++s) {
     const float* o = part + (((int64_t)n * nsl + s) * a.C + c) * 3;
     s1 += o[0];
@@ -1599,7 +1672,7 @@ int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, cons
   }
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gn_stat_partial_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, work);
-  hipLaunchKernelGGL(gn_stat_final_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, work, nsl, HW, C, N, stats);
+  hipLaunchKernelGGL(gn_stat_final_kernel, dim3(N * 32), dim3(64), 0, s, work, nsl, HW, C, N, stats);
   const int64_t tot = (int64_t)N * HW * C;
   hipLaunchKernelGGL(gn_apply_kernel, dim3(grid1(tot / 4)), dim3(TB), 0, s, x, tot, HW, C, stats, gamma, beta, ss,
                      ss_stride, act_silu, out);
