@@ -682,29 +682,42 @@ __global__ __launch_bounds__(64) void gn_stat_final_kernel(const double* __restr
 
 __device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + expf(-z)); }
 
-// 4 consecutive channels per thread (C % 32 == 0): one 16-B load / store and two 64-bit divisions per
-// 4 elements instead of per element (the per-element int64 div/mod made these passes VALU-bound)
-__global__ void gn_apply_kernel(const float* __restrict__ x, int64_t tot, int HW, int C, const float* __restrict__ stats,
-                                const float* __restrict__ gamma, const float* __restrict__ beta,
-                                const float* __restrict__ ss, int ss_stride, int act_silu, float* __restrict__ out) {
-  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-  if (i >= tot) return;
-  const int64_t pix = i / C;
-  const int c0 = (int)(i - pix * C);
-  const int n = (int)(pix / HW);
-  const int cpg = C / 32;
-  const f32x4 xv = *reinterpret_cast<const f32x4*>(x + i);
-  f32x4 o;
+// grid (slices, N), 256 threads in gn_stat_partial_kernel's (row, channel quad) layout: a thread keeps
+// its four channels' statistics, affine and scale/shift in registers and streams 16-B pixel quads
+__global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__ x, int HW, int C,
+                                                       const float* __restrict__ stats, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, const float* __restrict__ ss,
+                                                       int ss_stride, int act_silu, float* __restrict__ out) {
+  const int n = blockIdx.y;
+  const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, HW);
+  const int Q = C >> 2, R = 256 / Q;
+  const int q = threadIdx.x % Q, r = threadIdx.x / Q;
+  if (r >= R) return;
+  const int c0 = 4 * q, cpg = C / 32;
+  float mean[4], rstd[4], gam[4], bet[4], sc[4], sh[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = c0 + j;
-    const int g = c / cpg;
-    const float mean = stats[(n * 32 + g) * 2], rstd = stats[(n * 32 + g) * 2 + 1];
-    float z = (xv[j] - mean) * rstd * gamma[c] + beta[c];
-    if (ss) z = z * (1.0f + ss[(int64_t)n * ss_stride + c]) + ss[(int64_t)n * ss_stride + C + c];
-    o[j] = act_silu ? z * sigm(z) : z;
+    const int c = c0 + j, g = c / cpg;
+    mean[j] = stats[(n * 32 + g) * 2];
+    rstd[j] = stats[(n * 32 + g) * 2 + 1];
+    gam[j] = gamma[c];
+    bet[j] = beta[c];
+    sc[j] = ss ? 1.0f + ss[(int64_t)n * ss_stride + c] : 1.0f;
+    sh[j] = ss ? ss[(int64_t)n * ss_stride + C + c] : 0.0f;
   }
-  *reinterpret_cast<f32x4*>(out + i) = o;
+  const int64_t base = (int64_t)n * HW * C + c0;
+#pragma unroll 2
+  for (int p = p0 + r; p < p1; p += R) {
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(x + base + (int64_t)p * C);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float z = (xv[j] - mean[j]) * rstd[j] * gam[j] + bet[j];
+      if (ss) z = z * sc[j] + sh[j];
+      o[j] = act_silu ? z * sigm(z) : z;
+    }
+    *reinterpret_cast<f32x4*>(out + base + (int64_t)p * C) = o;
+  }
 }
 
 // GroupNorm(+ scale/shift)(+ SiLU) backward. With xhat = (x - mean) rstd, nrm = xhat gamma + beta,
@@ -718,27 +731,8 @@ struct GnBwdArgs {
   const float* gamma; const float* beta; const float* ss; int ss_stride; int act_silu;
   const float* stats;
 };
-__device__ __forceinline__ void gn_bwd_point(const GnBwdArgs& a, int n, int c, float xv, float dav, float& xhat,
-                                             float& nrm, float& dz, float& onep) {
-  const int g = c / (a.C / 32);
-  const float mean = a.stats[(n * 32 + g) * 2], rstd = a.stats[(n * 32 + g) * 2 + 1];
-  xhat = (xv - mean) * rstd;
-  nrm = xhat * a.gamma[c] + a.beta[c];
-  float z = nrm;
-  onep = 1.0f;
-  if (a.ss) {
-    onep = 1.0f + a.ss[(int64_t)n * a.ss_stride + c];
-    z = nrm * onep + a.ss[(int64_t)n * a.ss_stride + a.C + c];
-  }
-  if (a.act_silu) {
-    const float sg = sigm(z);
-    dz = dav * (sg * (1.0f + z * (1.0f - sg)));
-  } else {
-    dz = dav;
-  }
-}
 // grid (slices, N), 256 threads laid out as gn_stat_partial_kernel's (row, channel quad); a thread's
-// per-channel coefficients stay in registers and the per-point math is gn_bwd_point's
+// per-channel coefficients stay in registers
 __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnBwdArgs a, float* __restrict__ part) {
   // part [N][nsl][C][3]
   __shared__ float red[3][1024];  // [row][C] (R * C <= 1024), then per channel in row 0
@@ -849,30 +843,53 @@ __global__ void gn_bwd_param_kernel(GnBwdArgs a, const float* __restrict__ nc, f
   dgamma[c] += (float)g;
   dbeta[c] += (float)b;
 }
-__global__ void gn_bwd_dx_kernel(GnBwdArgs a, const float* __restrict__ red, float* __restrict__ dx, int accumulate) {
-  const int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);  // 4 channels per thread
-  const int64_t tot = (int64_t)a.N * a.HW * a.C;
-  if (i >= tot) return;
-  const int64_t pix = i / a.C;
-  const int c0 = (int)(i - pix * a.C);
-  const int n = (int)(pix / a.HW);
-  const f32x4 xv = *reinterpret_cast<const f32x4*>(a.x + i);
-  const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dout + i);
-  f32x4 prev = {0.f, 0.f, 0.f, 0.f};
-  if (accumulate) prev = *reinterpret_cast<const f32x4*>(dx + i);
-  f32x4 o;
+// grid (slices, N), the (row, channel quad) layout with per-channel coefficients in registers
+__global__ __launch_bounds__(256) void gn_bwd_dx_kernel(GnBwdArgs a, const float* __restrict__ red,
+                                                        float* __restrict__ dx, int accumulate) {
+  const int n = blockIdx.y, C = a.C;
+  const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, a.HW);
+  const int Q = C >> 2, R = 256 / Q;
+  const int q = threadIdx.x % Q, r = threadIdx.x / Q;
+  if (r >= R) return;
+  const int c0 = 4 * q, cpg = C / 32;
+  float mean[4], rstd[4], gam[4], bet[4], onep[4], sh[4], r0[4], r1[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = c0 + j;
-    float xhat, nrm, dz, onep;
-    gn_bwd_point(a, n, c, xv[j], dv[j], xhat, nrm, dz, onep);
-    const int g = c / (a.C / 32);
-    const float rstd = a.stats[(n * 32 + g) * 2 + 1];
-    const float dxhat = dz * onep * a.gamma[c];
-    const float v = rstd * (dxhat - red[(n * 32 + g) * 2] - xhat * red[(n * 32 + g) * 2 + 1]);
-    o[j] = accumulate ? prev[j] + v : v;
+    const int c = c0 + j, g = c / cpg;
+    mean[j] = a.stats[(n * 32 + g) * 2];
+    rstd[j] = a.stats[(n * 32 + g) * 2 + 1];
+    gam[j] = a.gamma[c];
+    bet[j] = a.beta[c];
+    onep[j] = a.ss ? 1.0f + a.ss[(int64_t)n * a.ss_stride + c] : 1.0f;
+    sh[j] = a.ss ? a.ss[(int64_t)n * a.ss_stride + C + c] : 0.0f;
+    r0[j] = red[(n * 32 + g) * 2];
+    r1[j] = red[(n * 32 + g) * 2 + 1];
   }
-  *reinterpret_cast<f32x4*>(dx + i) = o;
+  const int64_t base = (int64_t)n * a.HW * C + c0;
+#pragma unroll 2
+  for (int p = p0 + r; p < p1; p += R) {
+    const int64_t i = base + (int64_t)p * C;
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(a.x + i);
+    const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dout + i);
+    f32x4 prev = {0.f, 0.f, 0.f, 0.f};
+    if (accumulate) prev = *reinterpret_cast<const f32x4*>(dx + i);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // gn_bwd_partial_kernel's per-point arithmetic
+      const float xhat = (xv[j] - mean[j]) * rstd[j];
+      const float nrm = xhat * gam[j] + bet[j];
+      const float z = a.ss ? nrm * onep[j] + sh[j] : nrm;
+      float dz = dv[j];
+      if (a.act_silu) {
+        const float sg = sigm(z);
+        dz = dv[j] * (sg * (1.0f + z * (1.0f - sg)));
+      }
+      const float dxhat = dz * onep[j] * gam[j];
+      const float v = rstd[j] * (dxhat - r0[j] - xhat * r1[j]);
+      o[j] = accumulate ? prev[j] + v : v;
+    }
+    *reinterpret_cast<f32x4*>(dx + i) = o;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1673,8 +1690,7 @@ int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, cons
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gn_stat_partial_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, work);
   hipLaunchKernelGGL(gn_stat_final_kernel, dim3(N * 32), dim3(64), 0, s, work, nsl, HW, C, N, stats);
-  const int64_t tot = (int64_t)N * HW * C;
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid1(tot / 4)), dim3(TB), 0, s, x, tot, HW, C, stats, gamma, beta, ss,
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, stats, gamma, beta, ss,
                      ss_stride, act_silu, out);
   return TR_LAST();
 }
@@ -1684,8 +1700,8 @@ int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const
                   float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream) {
   const int nsl = (HW + GN_SL - 1) / GN_SL;
   const int64_t need = (int64_t)N * nsl * C * 3 + (int64_t)N * C * 3 + (int64_t)N * 64;
-  if (C % 32 || need > work_floats) {
-    set_error("ifd_tr_gn_bwd: C must be a multiple of 32; work too small");
+  if (C % 32 || C > 1024 || need > work_floats) {
+    set_error("ifd_tr_gn_bwd: C must be a multiple of 32 (<= 1024); work too small");
     return 2;
   }
   GnBwdArgs a{dout, x, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats};
@@ -1697,8 +1713,7 @@ int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const
   hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(grid1(N * C)), dim3(TB), 0, s, a, part, nsl, nc, dss);
   hipLaunchKernelGGL(gn_bwd_group_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, a, nc, red);
   hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
-  const int64_t tot = (int64_t)N * HW * C;
-  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(grid1(tot / 4)), dim3(TB), 0, s, a, red, dx, accumulate);
+  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl, N), dim3(256), 0, s, a, red, dx, accumulate);
   return TR_LAST();
 }
 
