@@ -1054,17 +1054,38 @@ __global__ __launch_bounds__(256) void attn_bwd_rows_kernel(const float* __restr
   const float* dob = dout + (int64_t)n * T * C;
   const int qo = head * 64, ko = C + head * 64, vo = 2 * C + head * 64;
   const float s2 = scale * scale;
-  for (int e = threadIdx.x; e < AB_R * T; e += blockDim.x) {
-    const int r = e / T, s = e % T, tq = r0 + r;
-    float acc = 0.f, accp = 0.f;
-    if (tq < T) {
-      for (int d = 0; d < 64; ++d) {
-        acc += (base[tq * row + qo + d] * scale) * (base[(int64_t)s * row + ko + d] * scale);
-        accp += dob[(int64_t)tq * C + head * 64 + d] * base[(int64_t)s * row + vo + d];
+  // S = (q scale)(k scale)^T and dP = do v^T: a thread owns key column s (its scaled k row and v row in
+  // registers, 16-B loads) and reads the block's q / do rows as LDS broadcasts
+  float* Qs = sh + 2 * AB_R * T;  // [AB_R][64] scaled q rows
+  float* Ds = Qs + AB_R * 64;     // [AB_R][64] do rows
+  for (int e = threadIdx.x; e < AB_R * 64; e += blockDim.x) {
+    const int r = e >> 6, d = e & 63, tq = r0 + r;
+    Qs[e] = tq < T ? base[(int64_t)tq * row + qo + d] * scale : 0.f;
+    Ds[e] = tq < T ? dob[(int64_t)tq * C + head * 64 + d] : 0.f;
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < T; s += blockDim.x) {
+    float kr[64], vr[64];
+#pragma unroll
+    for (int d4 = 0; d4 < 16; ++d4) {
+      const f32x4 kv = *reinterpret_cast<const f32x4*>(base + (int64_t)s * row + ko + 4 * d4);
+      const f32x4 vv = *reinterpret_cast<const f32x4*>(base + (int64_t)s * row + vo + 4 * d4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        kr[4 * d4 + j] = kv[j] * scale;
+        vr[4 * d4 + j] = vv[j];
       }
     }
-    S[e] = acc;
-    dP[e] = accp;
+    for (int r = 0; r < AB_R; ++r) {
+      float acc = 0.f, accp = 0.f;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) {
+        acc += Qs[r * 64 + d] * kr[d];
+        accp += Ds[r * 64 + d] * vr[d];
+      }
+      S[r * T + s] = acc;
+      dP[r * T + s] = accp;
+    }
   }
   __syncthreads();
   // softmax rows (fp32, max-subtracted), then dS
@@ -1099,13 +1120,21 @@ __global__ __launch_bounds__(256) void attn_bwd_rows_kernel(const float* __restr
       dSm[mo + e] = dP[e];
     }
   }
-  // dq[tq][d] = s2 sum_s dS[tq][s] k[s][d]
-  for (int e = threadIdx.x; e < AB_R * 64; e += blockDim.x) {
-    const int r = e / 64, d = e % 64, tq = r0 + r;
-    if (tq >= T) continue;
-    float acc = 0.f;
-    for (int s = 0; s < T; ++s) acc += dP[r * T + s] * base[(int64_t)s * row + ko + d];
-    dqkv[((int64_t)n * T + tq) * row + qo + d] = s2 * acc;
+  // dq[tq][d] = s2 sum_s dS[tq][s] k[s][d]: wave w takes rows w, w + 4, ..., lane = d, one k load per s
+  {
+    float acc[AB_R / 4];
+#pragma unroll
+    for (int i = 0; i < AB_R / 4; ++i) acc[i] = 0.f;
+    for (int s = 0; s < T; ++s) {
+      const float kv = base[(int64_t)s * row + ko + lane];
+#pragma unroll
+      for (int i = 0; i < AB_R / 4; ++i) acc[i] += dP[(wave + 4 * i) * T + s] * kv;
+    }
+#pragma unroll
+    for (int i = 0; i < AB_R / 4; ++i) {
+      const int tq = r0 + wave + 4 * i;
+      if (tq < T) dqkv[((int64_t)n * T + tq) * row + qo + lane] = s2 * acc[i];
+    }
   }
 }
 __global__ __launch_bounds__(256) void attn_bwd_cols_kernel(const float* __restrict__ qkv, const float* __restrict__ dout,
@@ -1119,16 +1148,27 @@ __global__ __launch_bounds__(256) void attn_bwd_cols_kernel(const float* __restr
   const int qo = head * 64, ko = C + head * 64, vo = 2 * C + head * 64;
   const float s2 = scale * scale;
   const int64_t mo = ((int64_t)n * nh + head) * T * T;
-  for (int e = threadIdx.x; e < AB_R * 64; e += blockDim.x) {
-    const int r = e / 64, d = e % 64, s = s0 + r;
-    if (s >= T) continue;
-    float dk = 0.f, dv = 0.f;
-    for (int t = 0; t < T; ++t) {
-      dk += dSm[mo + (int64_t)t * T + s] * base[(int64_t)t * row + qo + d];
-      dv += Pm[mo + (int64_t)t * T + s] * dob[(int64_t)t * C + head * 64 + d];
+  // wave w takes key rows s0 + w, s0 + w + 4, ..., lane = d: one q / do load per t serves them all
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dk[AB_R / 4], dv[AB_R / 4];
+#pragma unroll
+  for (int i = 0; i < AB_R / 4; ++i) dk[i] = dv[i] = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float qv = base[(int64_t)t * row + qo + lane];
+    const float dov = dob[(int64_t)t * C + head * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < AB_R / 4; ++i) {
+      const int s = min(s0 + wave + 4 * i, T - 1);
+      dk[i] += dSm[mo + (int64_t)t * T + s] * qv;
+      dv[i] += Pm[mo + (int64_t)t * T + s] * dov;
     }
-    dqkv[((int64_t)n * T + s) * row + ko + d] = s2 * dk;
-    dqkv[((int64_t)n * T + s) * row + vo + d] = dv;
+  }
+#pragma unroll
+  for (int i = 0; i < AB_R / 4; ++i) {
+    const int s = s0 + wave + 4 * i;
+    if (s >= T) continue;
+    dqkv[((int64_t)n * T + s) * row + ko + lane] = s2 * dk[i];
+    dqkv[((int64_t)n * T + s) * row + vo + lane] = dv[i];
   }
 }
 
@@ -1780,7 +1820,11 @@ int ifd_tr_attention_bwd(const float* qkv, const float* dout, int N, int T, int 
   float* Pm = scratch;
   float* dS = scratch + (int64_t)N * nh * T * T;
   dim3 g((T + AB_R - 1) / AB_R, nh, N);
-  const size_t lds = (size_t)2 * AB_R * T * sizeof(float);
+  const size_t lds = ((size_t)2 * AB_R * T + 2 * AB_R * 64) * sizeof(float);
+  if (lds > 160 * 1024) {
+    set_error("ifd_tr_attention_bwd: T too large for the row kernel's LDS");
+    return 2;
+  }
   static bool attr[kMaxDevices] = {};
   (void)set_lds_attr_once(attr, reinterpret_cast<const void*>(&attn_bwd_rows_kernel), (int)lds);
   hipStream_t s = (hipStream_t)stream;

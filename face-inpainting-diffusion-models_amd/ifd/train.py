@@ -502,8 +502,8 @@ class UNetTrainer:
             chk(lib().ifd_tr_attention_bwd(P(sv["qkv"]), P(da), N, T, C, sv["scale"], P(dqkv), P(scratch), sf, self.s))
             self.wgrad(dqkv, 3 * C, sv["n"], C, N, r, p + "qkv.weight", p + "qkv.bias")
             dn = self.conv(dqkv, 3 * C, N, r, p + "qkv.weight", transpose=True)
-            dx = self.gn_bwd(dn, sv["x"], N, T, C, p + "norm.", sv["st"], silu=False)
-            self.add_(dx, dout)
+            # the residual's gradient: accumulated into dout in place (dout is not read after this)
+            dx = self.gn_bwd(dn, sv["x"], N, T, C, p + "norm.", sv["st"], dx=dout, silu=False)
             return dx, r
         sv = saved[p]
         cin, cout, mode, r, ro = L["cin"], L["cout"], sv["mode"], sv["r"], sv["ro"]
@@ -518,16 +518,18 @@ class UNetTrainer:
         self.wgrad(dh1, cout, sv["a1r"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
         da1r = self.conv(dh1, cout, N, ro, p + "in_layers.2.weight", transpose=True)
         da1 = self.resample_bwd(da1r, N, r, cin, mode) if mode else da1r
-        dx = self.gn_bwd(da1, sv["x"], N, r * r, cin, p + "in_layers.0.", sv["st1"], silu=True)
         if cin != cout:
             self.wgrad(dout, cout, sv["xr"], cin, N, ro, p + "skip_connection.weight", p + "skip_connection.bias")
             dxr = self.conv(dout, cout, N, ro, p + "skip_connection.weight", transpose=True)
         else:
             dxr = dout
         if mode:
+            dx = self.gn_bwd(da1, sv["x"], N, r * r, cin, p + "in_layers.0.", sv["st1"], silu=True)
             self.resample_bwd(dxr, N, r, cin, mode, dx=dx)
         else:
-            self.add_(dx, dxr)
+            # the skip path's gradient (dout itself, or the 1x1 conv's fresh dgrad) is the accumulation
+            # target of the GroupNorm input gradient: no separate add pass
+            dx = self.gn_bwd(da1, sv["x"], N, r * r, cin, p + "in_layers.0.", sv["st1"], dx=dxr, silu=True)
         return dx, r
 
     # ------------------------------------------------------------------ loss / step
