@@ -1193,22 +1193,25 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ x
     y[wid] = post_silu ? v * sigm(v) : v;
   }
 }
-// dx[m][k] (+)= (sum_j dy[m][j] W[j][k]) * pre'(x[m][k]); block = 64 k x 4 j-quarters (merged in order)
-__global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict__ dy, const float* __restrict__ x,
-                                                        int M, int K, const float* __restrict__ w, int N, int pre_silu,
-                                                        float* __restrict__ dx, int accumulate) {
-  __shared__ float red[4][64];
+// dx[m][k] (+)= (sum_j dy[m][j] W[j][k]) * pre'(x[m][k]); block = 64 k x LDX_Q j-slices (merged in order)
+constexpr int LDX_Q = 16;
+__global__ __launch_bounds__(64 * LDX_Q) void linear_dx_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                               int M, int K, const float* __restrict__ w, int N,
+                                                               int pre_silu, float* __restrict__ dx, int accumulate) {
+  __shared__ float red[LDX_Q][64];
   const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int kblocks = (K + 63) / 64;
   const int m = blockIdx.x / kblocks, k = (blockIdx.x % kblocks) * 64 + kl;
   float part = 0.f;
   if (k < K)
-    for (int j = q; j < N; j += 4) part = fmaf(dy[(int64_t)m * N + j], w[(int64_t)j * K + k], part);
+    for (int j = q; j < N; j += LDX_Q) part = fmaf(dy[(int64_t)m * N + j], w[(int64_t)j * K + k], part);
   red[q][kl] = part;
   __syncthreads();
   if (q != 0 || k >= K) return;
   const int64_t i = (int64_t)m * K + k;
-  float acc = ((red[0][kl] + red[1][kl]) + red[2][kl]) + red[3][kl];
+  float acc = red[0][kl];
+#pragma unroll
+  for (int t = 1; t < LDX_Q; ++t) acc += red[t][kl];
   if (pre_silu) {
     const float v = x[i], sg = sigm(v);
     acc *= sg * (1.0f + v * (1.0f - sg));
@@ -1844,7 +1847,7 @@ int ifd_tr_linear_bwd(const float* dy, const float* x, int M, int K, const float
                       int dx_accumulate, float* dw, float* db, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dx)
-    hipLaunchKernelGGL(linear_dx_kernel, dim3(M * ((K + 63) / 64)), dim3(256), 0, s, dy, x, M, K, w, N, pre_silu, dx,
+    hipLaunchKernelGGL(linear_dx_kernel, dim3(M * ((K + 63) / 64)), dim3(64 * LDX_Q), 0, s, dy, x, M, K, w, N, pre_silu, dx,
                        dx_accumulate);
   if (dw)
     hipLaunchKernelGGL(linear_dw_kernel, dim3(grid1((int64_t)N * K)), dim3(TB), 0, s, dy, x, M, K, N, pre_silu, dw, db);

@@ -467,15 +467,15 @@ class UNetTrainer:
                 hcur = cin - sc
                 dprev = self._empty(N, r, r, hcur)
                 self.copy_ch(dh, cin, 0, dprev, hcur, 0, hcur, N * r * r, False)
-                ds_ = self._empty(N, r, r, sc)
-                self.copy_ch(dh, cin, hcur, ds_, sc, 0, sc, N * r * r, False)
-                dhs[hs_idx] = ds_
+                # the skip part stays in d cat until the input chain accumulates it (no copy of its own)
+                dhs[hs_idx] = (dh, cin, hcur, sc, N * r * r)
                 hs_idx += 1
                 dh = dprev
         # middle block's input = the last input block's output: dh continues down the input chain
         for bidx in range(len(in_blocks) - 1, -1, -1):
             section, bi, layers = in_blocks[bidx]
-            self.add_(dh, dhs[bidx])
+            dcat, cin, off, sc, npix = dhs[bidx]
+            self.copy_ch(dcat, cin, off, dh, sc, 0, sc, npix, True)
             for L in reversed(layers):
                 if L["kind"] == "conv_in":
                     self.wgrad(dh, L["cout"], tape["x16"], 16, N, r, L["prefix"] + "weight", L["prefix"] + "bias",
