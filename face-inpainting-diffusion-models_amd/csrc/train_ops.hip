@@ -656,6 +656,34 @@ __global__ __launch_bounds__(256) void gn_stat_partial_kernel(const float* __res
     o[1] = b;
   }
 }
+// (mean, rstd) per (n, g) from equal-count granule statistics gstat[n][C/4][E] = (mean, M2) of cnt
+// values each (the conv epilogue's / split-K reduction's): one wave per (n, g), float64 merges in a
+// fixed order (mean of the means, then M2 = sum M2_i + cnt sum (mean_i - mean)^2)
+__global__ __launch_bounds__(64) void gn_granule_final_kernel(const float* __restrict__ gstat, int E, float cnt, int C,
+                                                              float* __restrict__ stats) {
+  const int i = blockIdx.x;  // (n, g)
+  const int n = i / 32, g = i % 32;
+  const int qpg = C / 128;   // channel quads per group
+  const int K = qpg * E;
+  const float* base = gstat + ((int64_t)n * (C / 4) + (int64_t)g * qpg) * E * 2;  // the group's quads are adjacent
+  double a = 0.0;
+  for (int k = threadIdx.x; k < K; k += 64) a += base[2 * k];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+  const double mean = a / K;
+  double q = 0.0;
+  for (int k = threadIdx.x; k < K; k += 64) {
+    const double d = base[2 * k] - mean;
+    q += base[2 * k + 1] + (double)cnt * d * d;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+  if (threadIdx.x) return;
+  double var = q / ((double)K * cnt);
+  if (var < 0) var = 0;
+  stats[i * 2] = (float)mean;
+  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+}
 // one wave per (n, g): the lanes stride the slices, then a fixed butterfly (deterministic)
 __global__ __launch_bounds__(64) void gn_stat_final_kernel(const double* __restrict__ part, int nsl, int HW, int C,
                                                            int N, float* __restrict__ stats) {
@@ -1576,9 +1604,11 @@ int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int 
                              stream);
 }
 
-int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
-                        const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
-                        int64_t part_floats, unsigned* guard, int wx3_taps, void* stream) {
+static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
+                       const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
+                       int64_t part_floats, unsigned* guard, int wx3_taps, float* gstat, int64_t gstat_floats,
+                       int* gstat_E, float* gstat_cnt, void* stream) {
+  if (gstat_E) *gstat_E = 0;
   if ((H & (H - 1)) || c0 + c1 != cin_pad || !x0 || !out || !wx3 || !bias || !guard) {
     set_error("ifd_tr_conv_x3: unsupported arguments");
     return 2;
@@ -1603,10 +1633,59 @@ int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N,
     }
     p.part = part;
   }
+  // GroupNorm granule statistics of the output (when asked for and the geometry has them): from the
+  // epilogue of single-image 256-pixel tiles (E = 4 wave entries per tile, 256 values each), or from
+  // the split-K reduction (E = HW / min(HW, 64))
+  const int HW = H * H;
+  const int64_t skE = HW / (HW < 64 ? HW : 64);
+  const bool want = gstat && gstat_E && gstat_cnt && cout % 128 == 0;
+  if (want && p.ksplit == 1 && p.IMGS == 1 && p.TW * p.TH == 256 &&
+      (int64_t)N * (cout / 4) * p.tiles_x * p.tiles_y * 4 * 2 <= gstat_floats) {
+    p.gstat = gstat;
+    p.gstat_E = p.tiles_x * p.tiles_y * 4;
+  }
   int e = launch_conv_x3(p, XF_NONE, (hipStream_t)stream);
-  if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, (hipStream_t)stream);
+  if (!e && p.gstat) {
+    *gstat_E = p.gstat_E;
+    *gstat_cnt = 256.f;
+  }
+  if (!e && p.ksplit > 1) {
+    if (want && HW % (HW < 64 ? HW : 64) == 0 && (int64_t)N * (cout / 4) * skE * 2 <= gstat_floats) {
+      p.gstat = gstat;
+      int E = 0;
+      float cnt = 0.f;
+      e = launch_splitk_gstat(p, &E, &cnt, (hipStream_t)stream);
+      if (!e) {
+        *gstat_E = E;
+        *gstat_cnt = cnt;
+      }
+    } else {
+      e = launch_splitk_reduce(p, (hipStream_t)stream);
+    }
+  }
   if (e) set_error(std::string("ifd_tr_conv_x3: ") + hipGetErrorString((hipError_t)e));
   return e;
+}
+
+int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
+                        const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
+                        int64_t part_floats, unsigned* guard, int wx3_taps, void* stream) {
+  return conv_x3_run(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, wx3_taps,
+                     nullptr, 0, nullptr, nullptr, stream);
+}
+
+int64_t ifd_tr_gstat_floats(int N, int H, int cout) {
+  const int64_t HW = (int64_t)H * H;
+  const int64_t E = HW >= 64 ? HW / 64 : 1;
+  return (int64_t)N * (cout / 4) * E * 2;
+}
+
+int ifd_tr_conv_x3_gstat(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
+                         const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
+                         int64_t part_floats, unsigned* guard, int taps, float* gstat, int64_t gstat_floats,
+                         int* gstat_E, float* gstat_cnt, void* stream) {
+  return conv_x3_run(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, taps,
+                     gstat, gstat_floats, gstat_E, gstat_cnt, stream);
 }
 
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream) {
@@ -1735,6 +1814,21 @@ int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, cons
   hipLaunchKernelGGL(gn_stat_final_kernel, dim3(N * 32), dim3(64), 0, s, work, nsl, HW, C, N, stats);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, stats, gamma, beta, ss,
                      ss_stride, act_silu, out);
+  return TR_LAST();
+}
+
+int ifd_tr_gn_fwd_gstat(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
+                        int ss_stride, int act_silu, const float* gstat, int E, float cnt, float* out, float* stats,
+                        void* stream) {
+  if (C % 128 || C > 1024 || !gstat || E <= 0 || (double)E * cnt != 4.0 * HW) {
+    set_error("ifd_tr_gn_fwd_gstat: C must be a multiple of 128 (<= 1024) and E * cnt == 4 * HW");
+    return 2;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gn_granule_final_kernel, dim3(N * 32), dim3(64), 0, s, gstat, E, cnt, C, stats);
+  const int nsl = (HW + GN_SL - 1) / GN_SL;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, stats, gamma, beta, ss, ss_stride,
+                     act_silu, out);
   return TR_LAST();
 }
 

@@ -38,6 +38,10 @@ TRAIN_EXPORTS = {
     "ifd_tr_conv_x3_part_floats": (i64, [i32, i32, i32, i32]),
     "ifd_tr_conv_x3": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, vp]),
     "ifd_tr_conv_x3_taps": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp]),
+    "ifd_tr_gstat_floats": (i64, [i32, i32, i32]),
+    "ifd_tr_conv_x3_gstat": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, i64,
+                                   vp, vp, vp]),
+    "ifd_tr_gn_fwd_gstat": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, i32, f32, vp, vp, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
@@ -141,6 +145,7 @@ class UNetTrainer:
         self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
         self._grad_clean = False
         self._pack_cache = {}
+        self._gstat = {}
 
     # ------------------------------------------------------------------ parameters
     def p(self, name):
@@ -226,8 +231,19 @@ class UNetTrainer:
         out = self._empty(N, H, H, ppad)
         pf = lib().ifd_tr_conv_x3_part_floats(N, H, cin_pad, ppad)
         part = self._empty(max(pf, 1))
-        rc = lib().ifd_tr_conv_x3_taps(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, ppad, P(res), P(out),
-                                       P(part), pf, P(self._guard), taps, self.s)
+        if not transpose and ppad == pout and pout % 128 == 0:
+            # forward convs also hand the following GroupNorm its statistics (granules from the epilogue)
+            gf = lib().ifd_tr_gstat_floats(N, H, pout)
+            gstat = self._empty(gf)
+            E, cnt = _c.c_int(0), _c.c_float(0.0)
+            rc = lib().ifd_tr_conv_x3_gstat(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, ppad, P(res), P(out),
+                                            P(part), pf, P(self._guard), taps, P(gstat), gf, _c.byref(E),
+                                            _c.byref(cnt), self.s)
+            if rc == 0 and E.value > 0:
+                self._gstat[out.data_ptr()] = (out, gstat, E.value, cnt.value)
+        else:
+            rc = lib().ifd_tr_conv_x3_taps(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, ppad, P(res), P(out),
+                                           P(part), pf, P(self._guard), taps, self.s)
         if rc == 3:
             return None
         chk(rc)
@@ -289,6 +305,11 @@ class UNetTrainer:
     def gn_fwd(self, x, N, HW, C, prefix, ss=None, ss_stride=0, silu=True):
         out = self._empty(N * HW * C)
         stats = self._empty(N * 64)
+        g = self._gstat.get(x.data_ptr())
+        if g is not None and g[0] is x and C % 128 == 0:  # statistics from the producing conv's granules
+            chk(lib().ifd_tr_gn_fwd_gstat(P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")),
+                                          P(ss), ss_stride, int(silu), P(g[1]), g[2], g[3], P(out), P(stats), self.s))
+            return out, stats
         nsl = (HW + 255) // 256
         work = torch.empty(N * nsl * 64, device=self.dev, dtype=torch.float64)
         chk(lib().ifd_tr_gn_fwd(P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")), P(ss),
@@ -348,6 +369,7 @@ class UNetTrainer:
         cfg = self.cfg
         N, _, H, _ = x.shape
         self._pack_cache = {}
+        self._gstat = {}
         self.s = _lib.stream_ptr(self.dev)
         tape = {"N": N, "H": H}
         # time embedding: temb -> Linear -> SiLU -> Linear (unet.py:44-48); all emb_layers (nn.py:167-170)
@@ -654,11 +676,13 @@ class BlockTrainer(UNetTrainer):
         self.grad = torch.zeros(n, device=self.dev)
         self._zero_bias = torch.zeros(4096, device=self.dev)
         self._pack_cache = {}
+        self._gstat = {}
         self.precision, self.x3_dgrad, self.x3_loss_scale_log2, self.guard_trips = "fp32", False, 0, 0
         self.x3_wgrad = False
         self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
         self._grad_clean = False
         self._pack_cache = {}
+        self._gstat = {}
         self.s = None
 
     def load_state_dict(self, sd):
@@ -669,6 +693,7 @@ class BlockTrainer(UNetTrainer):
     def forward_block(self, x, emb=None):
         self.s = _lib.stream_ptr(self.dev)
         self._pack_cache = {}
+        self._gstat = {}
         N, C, H, _ = x.shape
         xh = x.to(self.dev, torch.float32).permute(0, 2, 3, 1).contiguous()
         self._saved = {}

@@ -52,6 +52,16 @@ int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int 
 int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
                         const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
                         int64_t part_floats, unsigned* guard, int taps, void* stream);
+/* ifd_tr_conv_x3_taps that also writes the output's GroupNorm granule statistics when the launch geometry
+ * has them (cout % 128 == 0; single-image 256-pixel tiles or a split-K reduction): gstat[n][cout/4][E] =
+ * (mean, M2) of *gstat_cnt values each; *gstat_E = E, or 0 when none were written (then use ifd_tr_gn_fwd).
+ * gstat needs ifd_tr_gstat_floats(N, H, cout) floats. Replaces the statistics pass of the GroupNorm that
+ * follows a conv (code/unet.py ResBlock in_layers / out_layers). */
+int64_t ifd_tr_gstat_floats(int N, int H, int cout);
+int ifd_tr_conv_x3_gstat(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
+                         const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
+                         int64_t part_floats, unsigned* guard, int taps, float* gstat, int64_t gstat_floats,
+                         int* gstat_E, float* gstat_cnt, void* stream);
 /* x[i] *= s (the loss scale of the 3xf16 backward and its removal from the gradients). */
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream);
 /* dw[cout][c0+c1][taps] += sum_pixels dy (x) shifted concat(x0, x1); db[cout] += column sums of dy. */
@@ -70,6 +80,11 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
 int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
                   int ss_stride, int act_silu, float* out, float* stats, double* work, int64_t work_doubles,
                   void* stream);
+/* ifd_tr_gn_fwd with the statistics merged from ifd_tr_conv_x3_gstat's granules of x (C % 128 == 0):
+ * no statistics pass over x. */
+int ifd_tr_gn_fwd_gstat(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
+                        int ss_stride, int act_silu, const float* gstat, int E, float cnt, float* out, float* stats,
+                        void* stream);
 /* its backward: dx (= or +=), dgamma/dbeta +=, dss (d scale, d shift) +=.
  * work: N*ceil(HW/256)*C*3 + N*C*3 + N*64 floats. */
 int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
