@@ -656,25 +656,32 @@ __global__ __launch_bounds__(256) void gn_stat_partial_kernel(const float* __res
     o[1] = b;
   }
 }
-// (mean, rstd) per (n, g) from equal-count granule statistics gstat[n][C/4][E] = (mean, M2) of cnt
-// values each (the conv epilogue's / split-K reduction's): one wave per (n, g), float64 merges in a
-// fixed order (mean of the means, then M2 = sum M2_i + cnt sum (mean_i - mean)^2)
-__global__ __launch_bounds__(64) void gn_granule_final_kernel(const float* __restrict__ gstat, int E, float cnt, int C,
+// (mean, rstd) per (n, g) from equal-count granule statistics of cnt values each (the conv epilogue's /
+// split-K reduction's): channels [0, C0) from g0[n][C0/4][E], [C0, C) from g1[n][(C-C0)/4][E] (a
+// concat's two sources) as (mean, M2). One wave per (n, g), float64 merges in a fixed order (mean of
+// the means, then M2 = sum M2_i + cnt sum (mean_i - mean)^2)
+__global__ __launch_bounds__(64) void gn_granule_final_kernel(const float* __restrict__ g0, int C0,
+                                                              const float* __restrict__ g1, int E, float cnt, int C,
                                                               float* __restrict__ stats) {
   const int i = blockIdx.x;  // (n, g)
   const int n = i / 32, g = i % 32;
   const int qpg = C / 128;   // channel quads per group
   const int K = qpg * E;
-  const float* base = gstat + ((int64_t)n * (C / 4) + (int64_t)g * qpg) * E * 2;  // the group's quads are adjacent
+  const int Q0 = C0 / 4, Q1 = (C - C0) / 4;
+  auto at = [&](int k) -> const float* {  // granule k of the group: quad g*qpg + k/E, entry k%E
+    const int qq = g * qpg + k / E, e = k % E;
+    return qq < Q0 ? g0 + (((int64_t)n * Q0 + qq) * E + e) * 2 : g1 + (((int64_t)n * Q1 + qq - Q0) * E + e) * 2;
+  };
   double a = 0.0;
-  for (int k = threadIdx.x; k < K; k += 64) a += base[2 * k];
+  for (int k = threadIdx.x; k < K; k += 64) a += at(k)[0];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
   const double mean = a / K;
   double q = 0.0;
   for (int k = threadIdx.x; k < K; k += 64) {
-    const double d = base[2 * k] - mean;
-    q += base[2 * k + 1] + (double)cnt * d * d;
+    const float* v = at(k);
+    const double d = v[0] - mean;
+    q += v[1] + (double)cnt * d * d;
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
@@ -1818,14 +1825,15 @@ int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, cons
 }
 
 int ifd_tr_gn_fwd_gstat(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
-                        int ss_stride, int act_silu, const float* gstat, int E, float cnt, float* out, float* stats,
-                        void* stream) {
-  if (C % 128 || C > 1024 || !gstat || E <= 0 || (double)E * cnt != 4.0 * HW) {
-    set_error("ifd_tr_gn_fwd_gstat: C must be a multiple of 128 (<= 1024) and E * cnt == 4 * HW");
+                        int ss_stride, int act_silu, const float* gstat0, int C0, const float* gstat1, int E,
+                        float cnt, float* out, float* stats, void* stream) {
+  if (C % 128 || C > 1024 || !gstat0 || C0 % 4 || C0 <= 0 || C0 > C || (C0 < C && !gstat1) || E <= 0 ||
+      (double)E * cnt != 4.0 * HW) {
+    set_error("ifd_tr_gn_fwd_gstat: C must be a multiple of 128 (<= 1024), 0 < C0 <= C in quads, E * cnt == 4 * HW");
     return 2;
   }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gn_granule_final_kernel, dim3(N * 32), dim3(64), 0, s, gstat, E, cnt, C, stats);
+  hipLaunchKernelGGL(gn_granule_final_kernel, dim3(N * 32), dim3(64), 0, s, gstat0, C0, gstat1, E, cnt, C, stats);
   const int nsl = (HW + GN_SL - 1) / GN_SL;
   hipLaunchKernelGGL(gn_apply_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, stats, gamma, beta, ss, ss_stride,
                      act_silu, out);

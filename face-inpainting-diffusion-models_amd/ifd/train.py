@@ -41,7 +41,7 @@ TRAIN_EXPORTS = {
     "ifd_tr_gstat_floats": (i64, [i32, i32, i32]),
     "ifd_tr_conv_x3_gstat": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, i64,
                                    vp, vp, vp]),
-    "ifd_tr_gn_fwd_gstat": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, i32, f32, vp, vp, vp]),
+    "ifd_tr_gn_fwd_gstat": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, i32, vp, i32, f32, vp, vp, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
@@ -240,7 +240,7 @@ class UNetTrainer:
                                             P(part), pf, P(self._guard), taps, P(gstat), gf, _c.byref(E),
                                             _c.byref(cnt), self.s)
             if rc == 0 and E.value > 0:
-                self._gstat[out.data_ptr()] = (out, gstat, E.value, cnt.value)
+                self._gstat[out.data_ptr()] = (out, gstat, E.value, cnt.value, pout, None)
         else:
             rc = lib().ifd_tr_conv_x3_taps(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, ppad, P(res), P(out),
                                            P(part), pf, P(self._guard), taps, self.s)
@@ -306,9 +306,10 @@ class UNetTrainer:
         out = self._empty(N * HW * C)
         stats = self._empty(N * 64)
         g = self._gstat.get(x.data_ptr())
-        if g is not None and g[0] is x and C % 128 == 0:  # statistics from the producing conv's granules
+        if g is not None and g[0] is x and C % 128 == 0:  # statistics from the producing conv(s)' granules
             chk(lib().ifd_tr_gn_fwd_gstat(P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")),
-                                          P(ss), ss_stride, int(silu), P(g[1]), g[2], g[3], P(out), P(stats), self.s))
+                                          P(ss), ss_stride, int(silu), P(g[1]), g[4], P(g[5]), g[2], g[3], P(out),
+                                          P(stats), self.s))
             return out, stats
         nsl = (HW + 255) // 256
         work = torch.empty(N * nsl * 64, device=self.dev, dtype=torch.float64)
@@ -390,6 +391,11 @@ class UNetTrainer:
                 cat = self._empty(N, hr, hr, hc + sc)
                 self.copy_ch(h, hc, 0, cat, hc + sc, 0, hc, N * hr * hr, False)
                 self.copy_ch(skip, sc, 0, cat, hc + sc, hc, sc, N * hr * hr, False)
+                # the concat's GroupNorm statistics from both sources' granules (same map: same E, cnt)
+                ga, gb = self._gstat.get(h.data_ptr()), self._gstat.get(skip.data_ptr())
+                if (ga is not None and gb is not None and ga[0] is h and gb[0] is skip and ga[5] is None
+                        and gb[5] is None and ga[2:4] == gb[2:4]):
+                    self._gstat[cat.data_ptr()] = (cat, ga[1], ga[2], ga[3], hc, gb[1])
                 h, hc = cat, hc + sc
             for L in layers:
                 k, p = L["kind"], L["prefix"]

@@ -80,11 +80,12 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
 int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
                   int ss_stride, int act_silu, float* out, float* stats, double* work, int64_t work_doubles,
                   void* stream);
-/* ifd_tr_gn_fwd with the statistics merged from ifd_tr_conv_x3_gstat's granules of x (C % 128 == 0):
- * no statistics pass over x. */
+/* ifd_tr_gn_fwd with the statistics merged from ifd_tr_conv_x3_gstat's granules of x (C % 128 == 0): no
+ * statistics pass over x. x = concat(a[C0], b[C - C0]) (the output blocks' skip concat) takes a's granules
+ * in gstat0 and b's in gstat1 (equal E and cnt); a single source passes C0 = C, gstat1 = NULL. */
 int ifd_tr_gn_fwd_gstat(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
-                        int ss_stride, int act_silu, const float* gstat, int E, float cnt, float* out, float* stats,
-                        void* stream);
+                        int ss_stride, int act_silu, const float* gstat0, int C0, const float* gstat1, int E,
+                        float cnt, float* out, float* stats, void* stream);
 /* its backward: dx (= or +=), dgamma/dbeta +=, dss (d scale, d shift) +=.
  * work: N*ceil(HW/256)*C*3 + N*C*3 + N*64 floats. */
 int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
