@@ -8,9 +8,11 @@ reference architecture (seeded manifest), gt ~ U(-1,1), 25 % centre-square + ran
 N GPUs = N independent shards (weak scaling), one RCCL all_gather of the outputs inside the
 timed region. `--gpus N` without a torch.distributed.run environment starts N ranks itself (a
 torch.distributed.run child launched before this process touches the GPU) and relays rank 0's
-line. `--noise parity` draws every noise tensor for the whole global batch on the host in the
-reference's order and keeps the rank's rows (SURVEY §8e: results independent of the GPU count);
-the default `device` mode draws per rank on the GPU (the throughput configuration).
+line. `--noise parity` draws every noise tensor for the whole global batch in the reference's order
+on the rank's GPU (the reference draws on the model's device, code/test_inp_ddim_100.py:481,554,567;
+every rank seeds the device generator identically, so the full-batch draw is the same on every rank)
+and keeps the rank's rows (results independent of the GPU count, at the cost of
+generating N x the rank's noise on-device); the default `device` mode draws per rank (per-rank seeds).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--noise device|parity]
 """
@@ -115,6 +117,20 @@ def pmc_traffic(kernel):
             return {"traffic": k["hbm_bytes_per_launch"], "mfma_busy": k.get("mfma_busy_frac"),
                     "traffic_source": os.path.relpath(path, ROOT)}
     return {"traffic": None}
+
+
+def parallelism_note(ws):
+    """The parallel layout as it really ran: backend and distinct devices. Fewer GPUs than ranks (ranks
+    sharing a device over gloo) is a rehearsal of the N-rank path, not an N-GPU measurement."""
+    if ws == 1:
+        return "dp1 (one GPU)"
+    import torch.distributed as dist
+    backend = dist.get_backend() if dist.is_initialized() else "none"
+    ndev = min(ws, torch.cuda.device_count())
+    note = f"dp{ws} (image shards over {ndev} device(s), {backend} all_gather of outputs)"
+    if ndev < ws:
+        note += " REHEARSAL: ranks share devices, not an N-GPU result"
+    return note
 
 
 def _free_port():
@@ -289,7 +305,7 @@ def main():
     ap.add_argument("--workload", choices=["sample", "train", "ddpm"], default="sample",
                     help="sample: the headline DDIM-100 sampler (default); train: the training step (configs[4]); ddpm: DDPM-1000 at B=64 (configs[2])")
     ap.add_argument("--noise", choices=["device", "parity"], default="device",
-                    help="device: per-rank GPU RNG (throughput); parity: full-batch host draws in reference order, "
+                    help="device: per-rank GPU RNG (throughput); parity: full-batch device draws in reference order, "
                          "sliced per rank (GPU-count-independent results)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -321,7 +337,7 @@ def main():
     diffusion = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="cosine")
     if args.noise == "parity":
         lo, hi = parallel.shard_range(B * ws, rank, ws)
-        sampler = InpaintingSampler(model, diffusion, ddim_timesteps=args.ddim_steps, device=dev, noise_device="cpu",
+        sampler = InpaintingSampler(model, diffusion, ddim_timesteps=args.ddim_steps, device=dev,
                                     noise_shard=(lo, hi, B * ws))
         gt, mask = (v[lo:hi].contiguous() for v in synth_inputs(B * ws, H, seed=7, device=dev))
     else:
@@ -407,7 +423,8 @@ def main():
         "metric": "256x256 DDIM-100 inpainted images/sec at 1/2/4/8 MI355X; per-step UNet ms",
         "value": round(value, 4),
         "unit": "images/s",
-        "n_gpus": ws,
+        "n_gpus": min(ws, torch.cuda.device_count()),
+        "n_ranks": ws,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2),
@@ -427,7 +444,7 @@ def main():
         "config": {"workload": "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1])",
                    "global_batch": B * ws, "batch_per_gpu": B, "unet_evals_per_image": n_evals,
                    "gflop_per_unet_eval_per_image": round(gflop_per_image(FULL), 2),
-                   "parallelism": f"dp{ws} (image shards, RCCL all_gather of outputs)"},
+                   "parallelism": parallelism_note(ws)},
         "roofline": roofline,
         "cpu_baseline": None,
     }

@@ -115,6 +115,12 @@ int ifd_memory(ifd_handle* h, int64_t* wb, int64_t* ws) {
   return 0;
 }
 
+int ifd_workspace_plan(ifd_handle* h, int64_t B, int64_t* ws) {
+  if (!h || !ws || B < 1 || B > (1 << 20)) { set_error("ifd_workspace_plan: bad argument"); return 2; }
+  *ws = h->model->workspace_bytes_for((int)B);
+  return 0;
+}
+
 int ifd_profile_enable(ifd_handle* h, int on) {
   if (!h) { set_error("null handle"); return 2; }
   return h->model->profile_enable(on);

@@ -339,7 +339,9 @@ __global__ __launch_bounds__(GN_NT) void gn_finalize2_kernel(GnFinalize2Params p
   block_sum64x3(sn, sm, sq, sh);
   const double ntot = sn;
   const double mean = sm / ntot;
-  const double m2 = sq - ntot * mean * mean;
+  // one-pass M2 in fp64 can cancel below zero for a group whose mean dwarfs its spread: clamp (as the
+  // training merge gn_granule_final_kernel does) so rstd stays finite
+  const double m2 = fmax(sq - ntot * mean * mean, 0.0);
   const float meanf = (float)mean;
   const float rstd = (float)(1.0 / sqrt(m2 / ntot + (double)p.eps));
   for (int c = g * Cg + tid; c < (g + 1) * Cg; c += GN_NT) {

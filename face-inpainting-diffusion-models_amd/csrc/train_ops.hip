@@ -1397,20 +1397,22 @@ __global__ void clip_coef_kernel(const double* __restrict__ part, int nb, float 
   out[0] = norm;
   out[1] = coef < 1.0f ? coef : 1.0f;
 }
+// scalars pre-formed on the host in double and rounded once (torch's AdamW: Python-float arithmetic,
+// then a float scalar per tensor op): decay = 1 - lr wd, w1 = 1 - b1, b2, w2 = 1 - b2, step = lr / bc1
 __global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
-                             int64_t n, const float* __restrict__ clip, float lr, float b1, float b2, float eps,
-                             float wd, float bc1, float bc2s) {
+                             int64_t n, const float* __restrict__ clip, float decay, float w1, float b2, float w2,
+                             float step, float eps, float bc2s) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float gi = g[i] * clip[1];
   g[i] = gi;
-  float pi = p[i] * (1.0f - lr * wd);
-  const float mi = m[i] + (gi - m[i]) * (1.0f - b1);  // torch lerp_
-  const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+  float pi = p[i] * decay;
+  const float mi = m[i] + (gi - m[i]) * w1;  // torch lerp_ (weight < 0.5 branch)
+  const float vi = v[i] * b2 + w2 * gi * gi;
   m[i] = mi;
   v[i] = vi;
   const float denom = sqrtf(vi) / bc2s + eps;
-  pi = pi - (lr / bc1) * (mi / denom);
+  pi = pi - step * (mi / denom);
   p[i] = pi;
 }
 
@@ -1993,16 +1995,16 @@ int ifd_tr_masked_mse(const float* out6_nhwc, int cs, const float* noise, const 
   return TR_LAST();
 }
 
-int ifd_tr_clip_adamw(float* p, float* g, float* m, float* v, int64_t n, float max_norm, float lr, float b1, float b2,
-                      float eps, float wd, int step, double* work, float* norm_coef, void* stream) {
+int ifd_tr_clip_adamw(float* p, float* g, float* m, float* v, int64_t n, float max_norm, double lr, double b1, double b2,
+                      double eps, double wd, int step, double* work, float* norm_coef, void* stream) {
   if (step < 1 || !work || !norm_coef) { set_error("ifd_tr_clip_adamw: bad arguments"); return 2; }
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(sumsq_partial_kernel, dim3(SQ_BLOCKS), dim3(256), 0, s, g, n, work);
   hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(64), 0, s, work, SQ_BLOCKS, max_norm, norm_coef);
-  const float bc1 = 1.0f - (float)std::pow((double)b1, step);
-  const float bc2s = (float)std::sqrt(1.0 - std::pow((double)b2, step));
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid1(n)), dim3(TB), 0, s, p, g, m, v, n, norm_coef, lr, b1, b2, eps, wd, bc1,
-                     bc2s);
+  const double bc1 = 1.0 - std::pow(b1, step);
+  const float bc2s = (float)std::sqrt(1.0 - std::pow(b2, step));
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid1(n)), dim3(TB), 0, s, p, g, m, v, n, norm_coef, (float)(1.0 - lr * wd),
+                     (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), (float)(lr / bc1), (float)eps, bc2s);
   return TR_LAST();
 }
 

@@ -75,6 +75,8 @@ class Model {
   int profile_filter(const char* prefix);  // record only launches whose name starts with prefix ("" = all)
   int profile_report(std::string& json);
   int64_t workspace_bytes() const { return (int64_t)ws_floats_ * 4; }
+  // arena size a forward at batch B would allocate (host-side plan, no device memory touched)
+  int64_t workspace_bytes_for(int B) const;
   // Conv arithmetic: IFD_PREC_FP32 (exact fp32 MFMA) or IFD_PREC_3XF16 (split f16 MFMA, fp32-accurate)
   int set_precision(int prec);
   int precision() const { return prec_; }
@@ -146,11 +148,15 @@ class Model {
   size_t ws_floats_ = 0;
   int ws_B_ = 0;
   // workspace carve (float offsets), valid for ws_B_
-  size_t o_x0_ = 0, o_bufs_[3] = {0, 0, 0}, o_t1_ = 0, o_qkv_ = 0, o_ao_ = 0, o_A_ = 0, o_B_ = 0, o_part_ = 0,
-         o_emb_ = 0, o_h1_ = 0, o_E_ = 0, o_split_ = 0, o_pool_ = 0, o_pool2_ = 0;
-  size_t split_floats_ = 0;
-  size_t pool_floats_ = 0;
-  std::vector<size_t> o_hs_;
+  struct WsLayout {
+    size_t o_x0_ = 0, o_bufs_[3] = {0, 0, 0}, o_t1_ = 0, o_qkv_ = 0, o_ao_ = 0, o_A_ = 0, o_B_ = 0, o_part_ = 0,
+           o_emb_ = 0, o_h1_ = 0, o_E_ = 0, o_split_ = 0, o_pool_ = 0, o_pool2_ = 0;
+    size_t split_floats_ = 0;  // split-K slab capacity
+    size_t pool_floats_ = 0;   // act_pool / act_apply staging capacity
+    std::vector<size_t> o_hs_;
+  };
+  WsLayout ly_;
+  size_t plan_workspace(int B, WsLayout& w, std::vector<std::pair<size_t, size_t>>& stat_of) const;
   // GroupNorm granule statistics: one area per activation buffer (hs, bufs, t1); stat_ holds the
   // buffers whose current contents have valid statistics (reset per forward)
   std::map<const float*, float*> stat_area_;

@@ -577,8 +577,9 @@ int Model::finalize() {
   return 0;
 }
 
-int Model::ensure_workspace(int B) {
-  if (ws_ && B <= ws_B_) return 0;
+// Workspace arena plan at batch B (host arithmetic only, no device calls): float offsets of every
+// area, and the (activation buffer, granule-statistics area) pairs. Returns the arena size in floats.
+size_t Model::plan_workspace(int B, WsLayout& w, std::vector<std::pair<size_t, size_t>>& stat_of) const {
   const int R = cfg_.image_size;
   size_t n = 0;
   auto reserve = [&](size_t cnt) {
@@ -587,10 +588,10 @@ int Model::ensure_workspace(int B) {
     return o;
   };
   size_t maxact = 0, maxqkv = 1, maxC = 16;
-  o_hs_.clear();
+  w.o_hs_.clear();
   for (size_t i = 0; i < in_ch_.size(); ++i) {
     const size_t sz = (size_t)B * in_res_[i] * in_res_[i] * in_ch_[i];
-    o_hs_.push_back(reserve(sz));
+    w.o_hs_.push_back(reserve(sz));
     maxact = std::max(maxact, sz);
   }
   for (auto& r : res_) {
@@ -616,18 +617,18 @@ int Model::ensure_workspace(int B) {
       if (L.kind == L_ATTN) maxqkv = std::max(maxqkv, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C * 3);
   for (auto& L : mid_)
     if (L.kind == L_ATTN) maxqkv = std::max(maxqkv, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C * 3);
-  o_x0_ = reserve((size_t)B * R * R * 16);
-  for (int k = 0; k < 3; ++k) o_bufs_[k] = reserve(maxact);
-  o_t1_ = reserve(maxact);
-  o_qkv_ = reserve(maxqkv);
-  o_ao_ = reserve(maxqkv / 3 + 1);
-  o_A_ = reserve((size_t)B * maxC);
-  o_B_ = reserve((size_t)B * maxC);
+  w.o_x0_ = reserve((size_t)B * R * R * 16);
+  for (int k = 0; k < 3; ++k) w.o_bufs_[k] = reserve(maxact);
+  w.o_t1_ = reserve(maxact);
+  w.o_qkv_ = reserve(maxqkv);
+  w.o_ao_ = reserve(maxqkv / 3 + 1);
+  w.o_A_ = reserve((size_t)B * maxC);
+  w.o_B_ = reserve((size_t)B * maxC);
   int slice;
   const int nsl = gn_slices(R * R, &slice);
-  o_part_ = reserve((size_t)B * nsl * 32 * 3);
+  w.o_part_ = reserve((size_t)B * nsl * 32 * 3);
   // split-K slabs: worst case over every conv of the plan at this batch
-  split_floats_ = 0;
+  w.split_floats_ = 0;
   auto consider = [&](const ConvW& cw, int H) {
     for (int x3 = 0; x3 < 2; ++x3) {  // fp32 kernels' geometry and the split kernel's
       ConvParams g;
@@ -637,21 +638,27 @@ int Model::ensure_workspace(int B) {
       const int nch = x3 ? x3_nchunks(cw) : cw.cin_pad / 8;
       conv_geometry(g, H, H, B, cw.bn, nch, x3 == 1);
       if (x3 && cw.taps == 1 && !cw.has_skip && g.ksplit == 1 && nch % 2 == 0) g.ksplit = 2;  // see run_conv
-      if (g.ksplit > 1) split_floats_ = std::max(split_floats_, (size_t)g.ksplit * B * H * H * cw.cout);
+      if (g.ksplit > 1) w.split_floats_ = std::max(w.split_floats_, (size_t)g.ksplit * B * H * H * cw.cout);
     }
   };
-  for (auto& r : res_) {
-    for (int H = 2; H <= R; H *= 2) {  // resolution is not stored per ResBlock: bound over all sizes
+  // only the (conv, output resolution) pairs the plan runs: every layer knows its input resolution
+  auto consider_layer = [&](const LayerP& L) {
+    if (L.kind == L_RES) {
+      const ResP& r = res_[L.idx];
+      const int H = r.xf == XF_UP ? 2 * L.res_in : (r.xf == XF_DOWN ? L.res_in / 2 : L.res_in);
       consider(r.conv1, H);
       consider(r.conv2, H);
+    } else {
+      consider(attn_[L.idx].qkv, L.res_in);
+      consider(attn_[L.idx].proj, L.res_in);
     }
-  }
-  for (auto& a : attn_)
-    for (int H = 2; H <= R; H *= 2) {
-      consider(a.qkv, H);
-      consider(a.proj, H);
-    }
-  o_split_ = reserve(std::max<size_t>(split_floats_, 64));
+  };
+  for (auto* blocks : {&in_blocks_, &out_blocks_})
+    for (auto& blk : *blocks)
+      for (auto& L : blk) consider_layer(L);
+  for (auto& L : mid_) consider_layer(L);
+  consider(conv_in_, R);
+  w.o_split_ = reserve(std::max<size_t>(w.split_floats_, 64));
   // act+pool staging of the down-ResBlocks (3xf16 mode): B x (res/2)^2 x cin, worst over the plan
   size_t maxpool = 64;
   for (auto& blk : in_blocks_)
@@ -665,27 +672,42 @@ int Model::ensure_workspace(int B) {
         if (L.kind == L_ATTN) maxpool = std::max(maxpool, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C);
   for (auto& L : mid_)
     if (L.kind == L_ATTN) maxpool = std::max(maxpool, (size_t)B * L.res_in * L.res_in * attn_[L.idx].C);
-  pool_floats_ = maxpool;
-  o_pool_ = reserve(maxpool);
-  o_pool2_ = reserve(maxpool);  // pooled residual (a down-ResBlock keeps cin == cout)
-  o_emb_ = reserve((size_t)B * emb_dim_);
-  o_h1_ = reserve((size_t)B * emb_dim_);
-  o_E_ = reserve((size_t)B * emb_total_);
+  w.pool_floats_ = maxpool;
+  w.o_pool_ = reserve(maxpool);
+  w.o_pool2_ = reserve(maxpool);  // pooled residual (a down-ResBlock keeps cin == cout)
+  w.o_emb_ = reserve((size_t)B * emb_dim_);
+  w.o_h1_ = reserve((size_t)B * emb_dim_);
+  w.o_E_ = reserve((size_t)B * emb_total_);
   // granule statistics areas: a tensor at resolution r with C channels has at most
   // max(r^2/64, 1) entries of C/4 (mean, M2) pairs per image
   auto stat_floats = [&](int r, int C) { return (size_t)B * std::max(r * r / 64, 1) * (C / 4) * 2; };
-  std::vector<std::pair<size_t, size_t>> stat_of;  // (buffer offset, stat offset)
-  for (size_t i = 0; i < o_hs_.size(); ++i) stat_of.push_back({o_hs_[i], reserve(stat_floats(in_res_[i], in_ch_[i]))});
+  stat_of.clear();  // (buffer offset, stat offset)
+  for (size_t i = 0; i < w.o_hs_.size(); ++i) stat_of.push_back({w.o_hs_[i], reserve(stat_floats(in_res_[i], in_ch_[i]))});
   size_t worst = 0;
   for (int r = 1; r <= R; r *= 2) worst = std::max(worst, stat_floats(r, (int)std::min<size_t>(maxC, 512)));
   worst = std::max(worst, stat_floats(R, 512));
-  for (int k = 0; k < 3; ++k) stat_of.push_back({o_bufs_[k], reserve(worst)});
-  stat_of.push_back({o_t1_, reserve(worst)});
+  for (int k = 0; k < 3; ++k) stat_of.push_back({w.o_bufs_[k], reserve(worst)});
+  stat_of.push_back({w.o_t1_, reserve(worst)});
+  return n;
+}
+
+int64_t Model::workspace_bytes_for(int B) const {
+  WsLayout w;
+  std::vector<std::pair<size_t, size_t>> stat_of;
+  return (int64_t)plan_workspace(B, w, stat_of) * 4;
+}
+
+int Model::ensure_workspace(int B) {
+  if (ws_ && B <= ws_B_) return 0;
+  WsLayout w;
+  std::vector<std::pair<size_t, size_t>> stat_of;
+  const size_t n = plan_workspace(B, w, stat_of);
   if (ws_) IFD_CHECK_HIP(hipFree(ws_));
   ws_ = nullptr;
   IFD_CHECK_HIP(hipMalloc(&ws_, n * sizeof(float)));
   ws_floats_ = n;
   ws_B_ = B;
+  ly_ = w;
   stat_area_.clear();
   for (auto& so : stat_of) stat_area_[ws_ + so.first] = ws_ + so.second;
   return 0;
@@ -722,8 +744,8 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   const int x3_chunks = x3_nchunks(cw);
   conv_geometry(p, H, H, N, cw.bn, x3_geo ? x3_chunks : cw.cin_pad / 8, x3_geo);
   if (epi != EPI_NHWC) p.ksplit = 1;
-  p.part = ws_ + o_split_;
-  IFD_REQUIRE(p.ksplit == 1 || (size_t)p.ksplit * N * H * H * cw.cout <= split_floats_, "split-K workspace");
+  p.part = ws_ + ly_.o_split_;
+  IFD_REQUIRE(p.ksplit == 1 || (size_t)p.ksplit * N * H * H * cw.cout <= ly_.split_floats_, "split-K workspace");
   if (sc) p.sc = *sc;
   p.img = img; p.gt = gt; p.mask = mask; p.noise = noise; p.known = known;
   IFD_REQUIRE(c0 % 8 == 0 && c1 % 8 == 0 && c0 + c1 == cw.cin_pad, "conv input channels");
@@ -747,16 +769,16 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
       xf == XF_NONE && !x3_masked_for(p)) {
     ConvParams q = p;
     q.in0 = nullptr; q.c0 = 0; q.in1 = nullptr; q.c1 = 0; q.cin_pad = 0; q.act = ACT_NONE;
-    q.s0 = act != ACT_NONE ? ws_ + o_pool_ : in0; q.sc0 = c0; q.s1 = nullptr; q.sc1 = 0;
+    q.s0 = act != ACT_NONE ? ws_ + ly_.o_pool_ : in0; q.sc0 = c0; q.s1 = nullptr; q.sc1 = 0;
     q.wskip = wblob_ + cw.x3s_off; q.cs_pad = cw.cin_pad;
     // a residual (proj_out) is added by the split-K reduction: the split kernel's 1x1 path has none
-    if (q.res && q.ksplit == 1 && x3_chunks % 2 == 0 && 2 * (size_t)N * H * H * cw.cout <= split_floats_) q.ksplit = 2;
+    if (q.res && q.ksplit == 1 && x3_chunks % 2 == 0 && 2 * (size_t)N * H * H * cw.cout <= ly_.split_floats_) q.ksplit = 2;
     if (conv_x3_eligible(q, 1, XF_NONE, cw.bn)) {
       if (act != ACT_NONE) {
-        IFD_REQUIRE((size_t)N * H * H * c0 <= pool_floats_, "act_apply workspace");
+        IFD_REQUIRE((size_t)N * H * H * c0 <= ly_.pool_floats_, "act_apply workspace");
         hipEvent_t pe;
         prof_begin(s, &pe, "act_pool");
-        const int e = launch_act_apply(in0, c0, N, H * H, act, A, Bc, ws_ + o_pool_, s);
+        const int e = launch_act_apply(in0, c0, N, H * H, act, A, Bc, ws_ + ly_.o_pool_, s);
         prof_end(s, pe, "act_pool", 0.0, 8.0 * N * (double)H * H * c0);
         IFD_REQUIRE(e == 0, "act_apply launch");
       }
@@ -767,7 +789,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   // 3xf16: the split kernel has no avg-pool prologue or residual; a down-ResBlock's convs read
   // act+pool(x) / pool(x) materialised by act_pool at the output resolution instead (the same
   // fp32 arithmetic as conv.hip's XF_DOWN paths)
-  // o_pool2_ holds pool(in0) only for the conv that directly follows the act_pool that wrote it
+  // ly_.o_pool2_ holds pool(in0) only for the conv that directly follows the act_pool that wrote it
   // (conv2 of the same down-ResBlock); any other conv in between invalidates it
   const float* pooled_prev = pooled_raw_;
   pooled_raw_ = nullptr;
@@ -776,12 +798,12 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     const bool pool_res = res && res_xf == XF_DOWN;
     ConvParams q = p;
     if (pool_in) {
-      q.in0 = ws_ + o_pool_;
+      q.in0 = ws_ + ly_.o_pool_;
       q.Hin = q.Win = H;
       q.act = ACT_NONE;
     }
     if (pool_res) {
-      q.res = ws_ + o_pool2_;
+      q.res = ws_ + ly_.o_pool2_;
       q.res_xform = XF_NONE;
       q.res_H = q.res_W = H;
     }
@@ -790,14 +812,14 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
       prof_begin(s, &pe, "act_pool");
       int e = 0;
       // conv1 of a down-ResBlock also pools its raw input for conv2's residual (same tensor, read
-      // once); conv2 then finds pool(res) already in o_pool2_
+      // once); conv2 then finds pool(res) already in ly_.o_pool2_
       if (pool_in) {
         const bool raw_too = c0 == cw.cout;  // a down-ResBlock keeps its width: conv2's residual is in0
-        e = launch_act_pool(in0, c0, N, Hin, act, A, Bc, ws_ + o_pool_, raw_too ? ws_ + o_pool2_ : nullptr, s);
+        e = launch_act_pool(in0, c0, N, Hin, act, A, Bc, ws_ + ly_.o_pool_, raw_too ? ws_ + ly_.o_pool2_ : nullptr, s);
         pooled_raw_ = raw_too ? in0 : nullptr;
       }
       if (!e && pool_res && res != pooled_prev)
-        e = launch_act_pool(res, cw.cout, N, resH, ACT_NONE, nullptr, nullptr, ws_ + o_pool2_, nullptr, s);
+        e = launch_act_pool(res, cw.cout, N, resH, ACT_NONE, nullptr, nullptr, ws_ + ly_.o_pool2_, nullptr, s);
       prof_end(s, pe, "act_pool", 0.0, 4.0 * N * (double)Hin * Hin * (c0 + (pool_res ? cw.cout : 0)) * 1.25);
       IFD_REQUIRE(e == 0, "act_pool launch");
       p = q;
@@ -958,7 +980,7 @@ int Model::run_gn(const float* in0, int c0, const float* in1, int c1, int N, int
                   int emb_stride, int emb_off, float* A, float* B, hipStream_t s) {
   if (!gn_fused_ || ((c0 + c1) / 32) % 4 != 0)  // granules are 4 channels: groups must hold whole ones
     return launch_gn(in0, c0, in1, c1, N, HW, wblob_ + gn.g_off, wblob_ + gn.b_off, emb, emb_stride, emb_off,
-                     ws_ + o_part_, A, B, s);
+                     ws_ + ly_.o_part_, A, B, s);
   StatRec r0, r1;
   if (stats_for(in0, c0, N, HW, &r0, s)) return 1;
   if (in1 && stats_for(in1, c1, N, HW, &r1, s)) return 1;
@@ -968,12 +990,12 @@ int Model::run_gn(const float* in0, int c0, const float* in1, int c1, int N, int
 
 int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, int c1, int N, int Hin, float* out,
                    hipStream_t s) {
-  float* A = ws_ + o_A_;
-  float* Bc = ws_ + o_B_;
-  float* part = ws_ + o_part_;
-  float* t1 = ws_ + o_t1_;
+  float* A = ws_ + ly_.o_A_;
+  float* Bc = ws_ + ly_.o_B_;
+  float* part = ws_ + ly_.o_part_;
+  float* t1 = ws_ + ly_.o_t1_;
   const int H = r.xf == XF_UP ? 2 * Hin : (r.xf == XF_DOWN ? Hin / 2 : Hin);
-  // o_pool2_'s pooled residual is valid only within the block whose conv1 wrote it
+  // ly_.o_pool2_'s pooled residual is valid only within the block whose conv1 wrote it
   pooled_raw_ = nullptr;
   hipEvent_t g0;
   prof_begin(s, &g0, "groupnorm_stats");
@@ -985,7 +1007,7 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
                0, t1, EPI_NHWC, s))
     return 1;
   prof_begin(s, &g0, "groupnorm_stats");
-  e = run_gn(t1, r.cout, nullptr, 0, N, H * H, r.gn2, ws_ + o_E_, emb_total_, r.emb_off, A, Bc, s);
+  e = run_gn(t1, r.cout, nullptr, 0, N, H * H, r.gn2, ws_ + ly_.o_E_, emb_total_, r.emb_off, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, H * H, r.cout));
   IFD_REQUIRE(e == 0, "gn launch");
   const float* res = r.conv2.has_skip ? nullptr : in0;
@@ -994,10 +1016,10 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
 }
 
 int Model::run_attn(const AttnP& a, const float* in, int N, int Hin, float* out, hipStream_t s) {
-  float* A = ws_ + o_A_;
-  float* Bc = ws_ + o_B_;
-  float* qkv = ws_ + o_qkv_;
-  float* ao = ws_ + o_ao_;
+  float* A = ws_ + ly_.o_A_;
+  float* Bc = ws_ + ly_.o_B_;
+  float* qkv = ws_ + ly_.o_qkv_;
+  float* ao = ws_ + ly_.o_ao_;
   const int T = Hin * Hin;
   hipEvent_t g0;
   prof_begin(s, &g0, "groupnorm_stats");
@@ -1031,28 +1053,28 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   }
   const int R = cfg_.image_size;
   const int mc = cfg_.model_channels;
-  float* x0 = ws_ + o_x0_;
+  float* x0 = ws_ + ly_.o_x0_;
   stat_.clear();
   pooled_raw_ = nullptr;
   hipEvent_t p0;
   prof_begin(s, &p0, "input_pack+temb+emb_proj");
   launch_pack_input(x, a, m, pack_mode, B, R * R, x0, s);
   launch_temb(t, wblob_ + freqs_, mc, wblob_ + te_w0_, wblob_ + te_b0_, wblob_ + te_w2_, wblob_ + te_b2_, emb_dim_, B,
-              ws_ + o_h1_, ws_ + o_emb_, s);
-  launch_emb_proj(ws_ + o_emb_, emb_dim_, B, wblob_ + embw_, wblob_ + embb_, emb_total_, ws_ + o_E_, s);
+              ws_ + ly_.o_h1_, ws_ + ly_.o_emb_, s);
+  launch_emb_proj(ws_ + ly_.o_emb_, emb_dim_, B, wblob_ + embw_, wblob_ + embb_, emb_total_, ws_ + ly_.o_E_, s);
   prof_end(s, p0, "input_pack+temb+emb_proj", 2.0 * B * (double)emb_dim_ * (mc + emb_dim_ + emb_total_),
            4.0 * B * (double)R * R * (7 + 16) + 4.0 * emb_dim_ * (double)emb_total_);
 
   // input blocks
   if (run_conv(conv_in_, x0, 16, nullptr, 0, B, R, R, XF_NONE, ACT_NONE, nullptr, nullptr, nullptr, 0, nullptr, 0,
-               nullptr, 0, 0, ws_ + o_hs_[0], EPI_NHWC, s))
+               nullptr, 0, 0, ws_ + ly_.o_hs_[0], EPI_NHWC, s))
     return 1;
-  const float* cur = ws_ + o_hs_[0];
+  const float* cur = ws_ + ly_.o_hs_[0];
   int cur_c = in_ch_[0], cur_r = in_res_[0];
   for (size_t i = 1; i < in_blocks_.size(); ++i) {
     const auto& L = in_blocks_[i];
     for (size_t k = 0; k < L.size(); ++k) {
-      float* dst = (k + 1 == L.size()) ? ws_ + o_hs_[i] : ws_ + o_bufs_[k % 2];
+      float* dst = (k + 1 == L.size()) ? ws_ + ly_.o_hs_[i] : ws_ + ly_.o_bufs_[k % 2];
       if (L[k].kind == L_RES) {
         const ResP& r = res_[L[k].idx];
         if (run_res(r, cur, cur_c, nullptr, 0, B, cur_r, dst, s)) return 1;
@@ -1068,7 +1090,7 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   int bi = 0;
   auto next_buf = [&](const float* avoid) {
     for (int k = 0; k < 3; ++k) {
-      float* b = ws_ + o_bufs_[(bi + k) % 3];
+      float* b = ws_ + ly_.o_bufs_[(bi + k) % 3];
       if (b != avoid) {
         bi = (bi + k + 1) % 3;
         return b;
@@ -1093,7 +1115,7 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
       if (L.kind == L_RES) {
         const ResP& r = res_[L.idx];
         if (k == 0) {
-          const float* skip = ws_ + o_hs_[hs_i];
+          const float* skip = ws_ + ly_.o_hs_[hs_i];
           if (run_res(r, cur, cur_c, skip, in_ch_[hs_i], B, cur_r, dst, s)) return 1;
           --hs_i;
         } else {
@@ -1108,8 +1130,8 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
     }
   }
   // out: GN -> SiLU -> conv 3x3 -> [B,6,H,W] (or the fused sampler update)
-  float* A = ws_ + o_A_;
-  float* Bc = ws_ + o_B_;
+  float* A = ws_ + ly_.o_A_;
+  float* Bc = ws_ + ly_.o_B_;
   prof_begin(s, &p0, "groupnorm_stats");
   int e = run_gn(cur, cur_c, nullptr, 0, B, R * R, gn_out_, nullptr, 0, 0, A, Bc, s);
   prof_end(s, p0, "groupnorm_stats", 0.0, gn_bytes(B, R * R, cur_c));

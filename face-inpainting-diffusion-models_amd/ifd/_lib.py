@@ -60,6 +60,7 @@ EXPORTS = {
     "ifd_load_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, c_i64p, ctypes.c_int]),
     "ifd_finalize": (ctypes.c_int, [ctypes.c_void_p]),
     "ifd_memory": (ctypes.c_int, [ctypes.c_void_p, c_i64p, c_i64p]),
+    "ifd_workspace_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, c_i64p]),
     "ifd_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     "ifd_guard_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ifd_guard_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]),

@@ -354,8 +354,8 @@ class GaussianDiffusion:
 
     def training_losses(self, model, x_start, t, model_kwargs=None, noise=None, use_injection=True,
                         injection_schedule="all", use_cumulative_noise=True):
-        """Masked eps-MSE (code/gaussian_diffusion.py:540-614). Forward only through the HIP UNet:
-        the backward pass (training) is not implemented in this round."""
+        """Masked eps-MSE (code/gaussian_diffusion.py:540-614) with any model callable (forward only;
+        the HIP training step with its backward is ifd.train.UNetTrainer.train_step)."""
         model_kwargs = model_kwargs or {}
         if noise is None:
             noise = self._randn_like(x_start)

@@ -14,11 +14,13 @@ Differences, all deliberate:
   * `precision` selects the conv arithmetic ("3xf16": the split mode, DESIGN.md §3a, whose error
     against exact arithmetic matches the reference's own fp32 — tests/test_gpu_full.py — and whose
     range guard recomputes any out-of-range eval in fp32; "fp32": the plain fp32 MFMA chain);
-    default from the IFD_PRECISION environment variable, else "3xf16", so the reference's scripts
-    can switch without edits.
+    default from the IFD_PRECISION environment variable, else "fp32" (the reference's own
+    arithmetic class, bit-comparable with earlier fp32 runs), so the reference's scripts can opt into
+    "3xf16" without edits. The active mode is logged (logger "ifd") when the model is created.
 """
 from __future__ import annotations
 
+import logging
 import math
 import os
 
@@ -41,7 +43,8 @@ def _unwrap(ckpt):
 def create_model_and_diffusion(checkpoint_path, device, img_size=256, *, steps=1000, noise_schedule="quadratic",
                                model_channels=128, seed=1, precision=None):
     cfg = UNetConfig(image_size=img_size, model_channels=model_channels)
-    precision = precision or os.environ.get("IFD_PRECISION", "3xf16")
+    precision = precision or os.environ.get("IFD_PRECISION", "fp32")
+    logging.getLogger("ifd").info("create_model_and_diffusion: conv arithmetic %s (IFD_PRECISION)", precision)
     model = DiffusionInpaintingModel(cfg, device=device, precision=precision)
     if checkpoint_path is None:
         sd = make_state_dict(cfg, seed=seed, prefix="base_model.")

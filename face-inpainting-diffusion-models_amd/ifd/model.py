@@ -103,6 +103,8 @@ class DiffusionInpaintingModel(torch.nn.Module):
         self._dirty = True
         self.dtype = torch.float32
         self.guard_trips = 0  # 3xf16 evals / loops recomputed in fp32 by the range guard
+        self._applied = None  # (handle, precision, options) last pushed to the library
+        self._deferred = None  # deferred_guard(): per-forward guard reads suspended
 
     # -- weights -------------------------------------------------------------------------------
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
@@ -132,10 +134,14 @@ class DiffusionInpaintingModel(torch.nn.Module):
                     del t
                 _lib.check(L.ifd_finalize(self._handle.h))
             self._dirty = False
-        L = _lib.lib()
-        _lib.check(L.ifd_set_precision(self._handle.h, _lib.PRECISIONS[self.precision]))
-        for k, v in self.options.items():
-            _lib.check(L.ifd_set_option(self._handle.h, k.encode(), int(v)))
+        # precision / options reach the handle only when they changed (no per-forward ctypes calls)
+        state = (id(self._handle), self.precision, tuple(sorted((k, int(v)) for k, v in self.options.items())))
+        if state != self._applied:
+            L = _lib.lib()
+            _lib.check(L.ifd_set_precision(self._handle.h, _lib.PRECISIONS[self.precision]))
+            for k, v in self.options.items():
+                _lib.check(L.ifd_set_option(self._handle.h, k.encode(), int(v)))
+            self._applied = state
         return self._handle
 
     # -- forward -------------------------------------------------------------------------------
@@ -170,10 +176,41 @@ class DiffusionInpaintingModel(torch.nn.Module):
             h.h, _lib.ptr(xx), _lib.ptr(mi), _lib.ptr(mk), _lib.ptr(tt), B, H, W, _lib.ptr(out), _lib.stream_ptr(dev))))
         return out
 
+    def deferred_guard(self):
+        """Context manager for a caller-driven loop of 3xf16 forwards (e.g. a reference script's own
+        per-step algebra around `model(...)`): the range guard is reset once on entry and read once
+        on exit instead of one stream sync per forward. A trip raises RuntimeError at exit (the
+        forwards' outputs were already consumed, so the caller re-runs the loop, e.g. with
+        precision="fp32"). Forwards inside the scope are not recomputed individually."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def scope():
+            if self.precision == "fp32" or self._deferred is not None:
+                yield
+                return
+            dev = self._handle_device or next(self.parameters()).device
+            h = self.handle(dev)
+            L = _lib.lib()
+            s = _lib.stream_ptr(dev)
+            _lib.check(L.ifd_guard_reset(h.h, s))
+            self._deferred = dev
+            try:
+                yield
+            finally:
+                self._deferred = None
+            tripped = ctypes.c_int()
+            _lib.check(L.ifd_guard_read(h.h, ctypes.byref(tripped), s))
+            if tripped.value:
+                self.guard_trips += 1
+                raise RuntimeError("ifd: 3xf16 range guard tripped inside deferred_guard(); re-run in fp32")
+        return scope()
+
     def run_guarded(self, h, dev, launch, before_retry=None):
         """Run `launch` (library calls on `h`); in 3xf16 mode check the range guard afterwards (one
-        stream sync) and, if it tripped, call `before_retry` and run `launch` again in exact fp32."""
-        if self.precision == "fp32":
+        stream sync) and, if it tripped, call `before_retry` and run `launch` again in exact fp32.
+        Inside deferred_guard() the check is left to the scope's exit."""
+        if self.precision == "fp32" or self._deferred is not None:
             return launch()
         L = _lib.lib()
         s = _lib.stream_ptr(dev)

@@ -63,7 +63,7 @@ TRAIN_EXPORTS = {
     "ifd_tr_pack_input": (i32, [vp, vp, vp, i32, i32, vp, vp]),
     "ifd_tr_q_sample_inject": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "ifd_tr_masked_mse": (i32, [vp, i32, vp, vp, i32, i32, vp, vp, vp, vp]),
-    "ifd_tr_clip_adamw": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, i32, vp, vp, vp]),
+    "ifd_tr_clip_adamw": (i32, [vp, vp, vp, vp, i64, f32] + [ctypes.c_double] * 5 + [i32, vp, vp, vp]),
 }
 
 _bound = None
@@ -145,7 +145,16 @@ class UNetTrainer:
         self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
         self._grad_clean = False
         self._pack_cache = {}
+        # GroupNorm granule statistics of forward activations, keyed by data_ptr: (tensor, stats, E, cnt,
+        # channels, second-source stats). Valid only while the tensor holds what its producing conv wrote:
+        # the `is` check guards against a reused address, and every in-place write to a tensor (the
+        # accumulating add_ / copy_ch / gn_bwd / resample_bwd paths) drops its entry (_dirty).
         self._gstat = {}
+
+    def _dirty(self, t):
+        """`t` is about to be written in place: its recorded statistics no longer describe it."""
+        if t is not None and self._gstat:
+            self._gstat.pop(t.data_ptr(), None)
 
     # ------------------------------------------------------------------ parameters
     def p(self, name):
@@ -321,6 +330,8 @@ class UNetTrainer:
         acc = dx is not None
         if dx is None:
             dx = self._empty(N * HW * C)
+        else:
+            self._dirty(dx)
         nsl = (HW + 255) // 256
         work = self._empty(N * nsl * C * 3 + N * C * 3 + N * 64)
         chk(lib().ifd_tr_gn_bwd(P(dout), P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")),
@@ -338,14 +349,18 @@ class UNetTrainer:
         acc = dx is not None
         if dx is None:
             dx = self._empty(N, Hin, Hin, C)
+        else:
+            self._dirty(dx)
         chk(lib().ifd_tr_resample_bwd(P(dy), N, Hin, C, mode, P(dx), int(acc), self.s))
         return dx
 
     def add_(self, dst, src):
+        self._dirty(dst)
         chk(lib().ifd_tr_add(P(dst), P(src), P(dst), dst.numel(), self.s))
         return dst
 
     def copy_ch(self, src, cs, soff, dst, cd, doff, nc, npix, acc):
+        self._dirty(dst)
         chk(lib().ifd_tr_copy_channels(P(src), cs, soff, P(dst), cd, doff, nc, npix, int(acc), self.s))
 
     def linear(self, x, M, name_w, name_b, pre_silu=False):

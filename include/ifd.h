@@ -108,6 +108,10 @@ int ifd_set_option(ifd_handle* h, const char* key, int value);
 int ifd_get_option(ifd_handle* h, const char* key, int* value);
 /* Bytes of device workspace the handle holds (weights + activations). */
 int ifd_memory(ifd_handle* h, int64_t* weight_bytes, int64_t* workspace_bytes);
+/* Bytes of activation workspace a forward at batch B would allocate (the arena plan: resident
+ * skip tensors, rotating block buffers, split-K slabs of the convs the plan runs, statistics).
+ * Host arithmetic only, no GPU use; the handle's current arena is not changed. */
+int ifd_workspace_plan(ifd_handle* h, int64_t B, int64_t* workspace_bytes);
 
 int ifd_unet_forward(ifd_handle* h, const float* x, const float* masked_image, const float* mask,
                      const int64_t* t, int64_t B, int H, int W, float* out6, void* stream);

@@ -126,8 +126,10 @@ int ifd_tr_masked_mse(const float* out6_nhwc, int cs, const float* noise, const 
                       float* loss, float* dout6_nhwc, float* work, void* stream);
 /* clip_grad_norm_(max_norm) then AdamW over one flat parameter buffer; norm_coef[0] = grad norm,
  * [1] = clip coefficient (device; no host sync). work: 1024 doubles. step >= 1. */
-int ifd_tr_clip_adamw(float* p, float* g, float* m, float* v, int64_t n, float max_norm, float lr, float b1, float b2,
-                      float eps, float wd, int step, double* work, float* norm_coef, void* stream);
+/* The optimizer's scalars arrive as doubles (Python floats): 1 - lr*wd, 1 - b1, 1 - b2, lr / (1 - b1^k) and
+ * sqrt(1 - b2^k) are formed in double and rounded to fp32 once, as torch's AdamW forms them. */
+int ifd_tr_clip_adamw(float* p, float* g, float* m, float* v, int64_t n, float max_norm, double lr, double b1, double b2,
+                      double eps, double wd, int step, double* work, float* norm_coef, void* stream);
 
 #ifdef __cplusplus
 }

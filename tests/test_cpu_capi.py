@@ -94,3 +94,25 @@ def test_resize_coeffs_match_oracle(n_in, n_out):
     assert L.ifd_resize_coeffs(n_in, n_out, b.ctypes.data_as(ctypes.c_void_p), k.ctypes.data_as(ctypes.c_void_p),
                                ctypes.byref(ks)) == 0
     assert np.array_equal(b.reshape(-1, 2), b_ref) and np.array_equal(k.reshape(n_out, -1), k_ref)
+
+
+def test_workspace_plan_is_activation_bound():
+    """The arena plan (host arithmetic, no GPU) reserves split-K slabs only for the (conv, resolution)
+    pairs the plan runs: ~4.1 GB at B=16 and ~16.6 GB at B=64 for the full 256x256 model (round 2
+    bounded every conv at every resolution: 67.9 GB at B=64, mostly qkv slabs sized for 256x256),
+    growing linearly with the batch; the handle's own arena is untouched (still empty)."""
+    from ifd import _lib
+    from ifd.model import Handle
+    from ifd.topology import FULL
+    h = Handle(FULL)
+    L = _lib.lib()
+    got = {}
+    for B in (1, 16, 64, 128):
+        v = ctypes.c_int64()
+        assert L.ifd_workspace_plan(h.h, B, ctypes.byref(v)) == 0
+        got[B] = v.value
+    assert got[16] <= 4.5e9 and got[64] <= 17.5e9
+    assert abs(got[128] / got[64] - 2.0) < 0.02
+    wb, ws = ctypes.c_int64(), ctypes.c_int64()
+    assert L.ifd_memory(h.h, ctypes.byref(wb), ctypes.byref(ws)) == 0 and ws.value == 0
+    assert L.ifd_workspace_plan(h.h, 0, ctypes.byref(ws)) != 0

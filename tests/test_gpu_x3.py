@@ -220,3 +220,22 @@ def test_x3_range_guard_loop(record):
             assert m.guard_trips == 1 and m.precision == "3xf16"
     record("x3_range_guard/loop", maxabs_vs_fp32=maxabs(outs["3xf16"], outs["fp32"]))
     assert torch.equal(outs["3xf16"], outs["fp32"])
+
+
+def test_x3_deferred_guard_scope(evals, x3_model):
+    """deferred_guard(): a caller-driven loop of 3xf16 forwards reads the guard once at the scope's
+    exit (no per-forward sync); in-range inputs pass, an out-of-range layer raises at exit."""
+    from ifd.model import DiffusionInpaintingModel
+    x, gt, mask = (_t(evals[f"full/{k}"]).to(DEV) for k in ("x", "gt", "mask"))
+    t = torch.tensor([999], device=DEV)
+    with torch.no_grad():
+        ref = x3_model(x, t, masked_image=gt * (1 - mask), mask=mask)
+        with x3_model.deferred_guard():
+            ys = [x3_model(x, t, masked_image=gt * (1 - mask), mask=mask) for _ in range(3)]
+    assert all(torch.equal(y, ref) for y in ys)
+    m3 = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16")
+    m3.load_state_dict(_scaled_state_dict())
+    with torch.no_grad(), pytest.raises(RuntimeError, match="deferred_guard"):
+        with m3.deferred_guard():
+            m3(x, t, masked_image=gt * (1 - mask), mask=mask)
+    assert m3.guard_trips == 1
