@@ -37,6 +37,8 @@
 //     s + 2 while chunk s is split and consumed.
 // LDS: A = 4 planes [part hi/lo][channel half h][halo px][8 f16] (<= 21.25 KiB) double-buffered,
 // W = [tap][part][h][64 co][8 f16] (36 KiB) in a 3-slot ring (DMA two chunks ahead).
+#include <type_traits>
+
 #include "conv.h"
 #include "conv_dev.h"
 
@@ -176,6 +178,11 @@ __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int
 
 #ifndef X3_PREF
 #define X3_PREF 2
+#endif
+// X3_DEFER=1: the non-skip instantiations store a unit's outputs during the next unit's chunks and load
+// its residual during its own last chunks (the consumer's deferred epilogue); 0: the round-2 epilogue
+#ifndef X3_DEFER
+#define X3_DEFER 1
 #endif
 #ifndef X3_PINF
 #define X3_PINF 1
@@ -398,8 +405,14 @@ __device__ __forceinline__ f32x16 xmfma(f16x8 a, f16x8 b, f32x16 c) {
 // MFMAs over one staged 3x3 chunk: 9 taps x (3 split products x 2 x 2 fragment blocks);
 // operand = the halo stage (planes of Geo::NP pixels, pb = halo pixel).
 // NPROD = 1 (the f16 precision mode): the hi x hi product only.
-template <int TW, int NPROD>
-__device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws, const int (&pb)[2]) {
+// `extra(tap)` (taps 0-7) issues the deferred epilogue's memory operations between the tap's first MFMA
+// group and its split-product groups, so they drain beside MFMAs instead of in a burst.
+struct XNoExtra {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+template <int TW, int NPROD, typename F = XNoExtra>
+__device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws, const int (&pb)[2],
+                                           F&& extra = F()) {
   using Geo = XGeo<TW>;
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const lds_f* Ah = As + 4 * (h * Geo::NP);
@@ -430,6 +443,8 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
         acc[mr][nr] = xmfma(ah[cur][mr], bs[cur][nr], acc[mr][nr]);
     __builtin_amdgcn_sched_barrier(0);
     if (tap + 1 < 9) fetch(tap + 1, cur ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (tap < 8) extra(tap);
     __builtin_amdgcn_sched_barrier(0);
     if (NPROD == 1) continue;
 #pragma unroll
@@ -539,44 +554,9 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
             }
       }
     };
-    auto epilogue = [&](const STile& t, int z, bool tstamp = false) {
-      if (X3_ABLATE == 13) {  // timing only: no epilogue
-        asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
-        return;
-      }
-      const size_t img = (size_t)p.H * p.W * p.cout;
-      const int vb = vbase(t);
-      if (S > 1) {  // raw partial sums into slab z (splitk_reduce adds the slabs, bias, residual)
-        const rsrc_t rp = mkrsrc(p.part + ((size_t)z * p.N + t.n0) * img);
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr)
-#pragma unroll
-          for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[mr][nr][r] * (1.0f / kLo)), rp,
-                                                    vb + mr * mstep + nr * 128, roff(r), 0);
-        return;
-      }
-      const rsrc_t ro = mkrsrc(p.out + (size_t)t.n0 * img);
-      // the outputs replace the accumulators (they are zeroed after the epilogue)
-#pragma unroll
-      for (int nr = 0; nr < 2; ++nr)
-#pragma unroll
-        for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float x = acc[mr][nr][r] * (1.0f / kLo);  // exact rescale
-            x = x + bias2[nr];
-            if (!SKIP && p.res) x = rv[mr][nr][r] + x;  // torch order: x_res + (conv + bias)
-            acc[mr][nr][r] = x;
-            if (X3_ABLATE != 14)
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep + nr * 128,
-                                                    roff(r), 0);
-          }
-      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
-        p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values + stores issued
-      if (X3_ABLATE != 15 && p.gstat) {
+    // GroupNorm granule statistics of the unit's output values v[mr][nr][r] (the accumulators after the
+    // epilogue arithmetic, or the deferred epilogue's rv)
+    auto gstats = [&](const STile& t, const auto& v) __attribute__((always_inline)) {
         // GroupNorm granule statistics of each output channel: over this lane's 32 pixels (two-pass),
         // then merged with the other column half (lane ^ 32) and over the channel quad (lanes ^ 1,
         // ^ 2). Every merge joins two equal counts, so Chan's update needs no division:
@@ -591,14 +571,14 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
 #pragma unroll
           for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sm += acc[mr][nr][r];
+            for (int r = 0; r < 16; ++r) sm += v[mr][nr][r];
           mean[nr] = sm * (1.0f / 32);
           float q = 0.f;
 #pragma unroll
           for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const float d = acc[mr][nr][r] - mean[nr];
+              const float d = v[mr][nr][r] - mean[nr];
               q += d * d;
             }
           m2[nr] = q;
@@ -636,7 +616,45 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
             o[1] = m2[nr];
           }
         }
+    };
+    auto epilogue = [&](const STile& t, int z, bool tstamp = false) {
+      if (X3_ABLATE == 13) {  // timing only: no epilogue
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
+        return;
       }
+      const size_t img = (size_t)p.H * p.W * p.cout;
+      const int vb = vbase(t);
+      if (S > 1) {  // raw partial sums into slab z (splitk_reduce adds the slabs, bias, residual)
+        const rsrc_t rp = mkrsrc(p.part + ((size_t)z * p.N + t.n0) * img);
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+          for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[mr][nr][r] * (1.0f / kLo)), rp,
+                                                    vb + mr * mstep + nr * 128, roff(r), 0);
+        return;
+      }
+      const rsrc_t ro = mkrsrc(p.out + (size_t)t.n0 * img);
+      // the outputs replace the accumulators (they are zeroed after the epilogue)
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float x = acc[mr][nr][r] * (1.0f / kLo);  // exact rescale
+            x = x + bias2[nr];
+            if (!SKIP && p.res) x = rv[mr][nr][r] + x;  // torch order: x_res + (conv + bias)
+            acc[mr][nr][r] = x;
+            if (X3_ABLATE != 14)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep + nr * 128,
+                                                    roff(r), 0);
+          }
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
+        p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values + stores issued
+      if (X3_ABLATE != 15 && p.gstat) gstats(t, acc);
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
         p.trace[64 * blockIdx.x + 45] = __builtin_amdgcn_s_memtime();  // statistics done
     };
@@ -741,6 +759,155 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     zero();
     XBARRIER_CONSUMER();  // chunk 0 staged
     int j = 0;  // position in the block's chunk stream: ring slot j % 3, A stage j & 1
+#if X3_DEFER
+    if (!SKIP && nchu >= 8) {
+      // Deferred epilogue (the non-skip instantiations whose units have >= 8 chunks; shorter units - the
+      // split-K and 8x8 layers, the input conv - keep the epilogue below: two phases of rv that overlap
+      // in one chunk would not fit the register budget). A unit's outputs (x 2^-11, bias, residual) are
+      // computed into rv at the unit's end - with its GroupNorm granule statistics - and STORED during
+      // the next unit's first chunks, two registers per tap between MFMA groups; the residual of a unit
+      // is LOADED into rv the same way during its last chunks. IFD_TRACE stamps (round 2, the 128-channel
+      // 256^2 layers) had the 64 dword stores per wave at ~3.4k cycles of a ~10k-cycle unit transition
+      // and the residual's 64 loads, issued in one burst, at +3.7k on their chunk: the CU's
+      // vector-memory issue rate, not the bytes. rv is the register set the epilogue already used.
+      const size_t img = (size_t)p.H * p.W * p.cout;
+      bool pending = false;  // rv holds the previous unit's outputs, not yet stored
+      rsrc_t rdst = mkrsrc(p.out), rres = mkrsrc(p.out);
+      int vbd = 0;
+      // XF_UP residual offsets, separable like roff: register (mr, r) of lane (h, l32) sits at output
+      // row wrow + (32 / TW) mr (+ (r >> 3) at TW = 16) and column 4 h + c(r), c(r) = (8 (r >> 2) + (r & 3))
+      // mod TW (4 h + c(r) < TW); tile origins are even, so the source pixel is row (y0 + wrow) / 2 + mr
+      // (TW = 16) or (y0 + wrow) / 2 (TW = 32), column x0 / 2 + 2 h + c(r) / 2
+      int vbu[2] = {0, 0};
+      auto uoff = [&](int r) { return (((8 * (r >> 2) + (r & 3)) & (TW - 1)) >> 1) * p.cout * 4; };
+      auto st1 = [&](int mr, int nr, int r) __attribute__((always_inline)) {
+        if (X3_ABLATE != 14)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rv[mr][nr][r]), rdst,
+                                                vbd + mr * mstep + nr * 128, roff(r), 0);
+      };
+      auto ld1 = [&](auto UP, int mr, int nr, int r) __attribute__((always_inline)) {
+        if (!decltype(UP)::value) {
+          rv[mr][nr][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rres, vbu[mr] + nr * 128, roff(r), 0));
+        } else {  // XF_UP: nearest-upsampled residual, lane part vbu[mr] + wave-uniform part uoff(r)
+          rv[mr][nr][r] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rres, vbu[mr] + nr * 128, uoff(r), 0));
+        }
+      };
+      // one chunk whose taps 0-7 also store pieces [QS, QS + NS) and load pieces [QL, QL + NL) of rv
+      // (piece q = block (q >> 1, q & 1), 16 registers, two per tap); LD is compile-time so that rv has
+      // one definition point per path (a merge of a loaded and an unloaded copy would cost a vmcnt wait)
+      auto chunk = [&](auto QS, auto NS, auto QL, auto NL, bool do_st, auto LD) __attribute__((always_inline)) {
+        constexpr int qs = decltype(QS)::value, ns = decltype(NS)::value;
+        constexpr int ql = decltype(QL)::value, nl = decltype(NL)::value;
+        constexpr int ld = decltype(LD)::value;  // 0 no loads, 1 identity residual, 2 nearest-up residual
+        auto extra = [&](int tap) __attribute__((always_inline)) {
+          if (ns > 0 && do_st) {
+#pragma unroll
+            for (int q = qs; q < qs + ns; ++q) {
+              st1(q >> 1, q & 1, 2 * tap);
+              st1(q >> 1, q & 1, 2 * tap + 1);
+            }
+          }
+          if (ld) {
+            using Up = std::integral_constant<bool, ld == 2>;
+#pragma unroll
+            for (int q = ql; q < ql + nl; ++q) {
+              ld1(Up(), q >> 1, q & 1, 2 * tap);
+              ld1(Up(), q >> 1, q & 1, 2 * tap + 1);
+            }
+          }
+        };
+        stamp(j);
+        if (X3_ABLATE != 4) consume_x3<TW, NPROD>(acc, A0 + (j & 1) * XA, W0 + (j % 3) * XW, pb, extra);
+        stamp(j, 16);
+        ++j;
+        XBARRIER_CONSUMER();
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      using I2 = std::integral_constant<int, 2>;
+      using I3 = std::integral_constant<int, 3>;
+      using NoLd = std::integral_constant<int, 0>;
+      auto run_units = [&](auto RES) __attribute__((always_inline)) {
+        constexpr int resk = decltype(RES)::value;  // S == 1 and a residual: 1 identity, 2 nearest-up
+        constexpr bool res = resk != 0;
+        using Ld = std::integral_constant<int, resk>;
+        for (int u = 0; u < nu; ++u) {
+          int z;
+          const STile t = unit_of(u, z);
+          const int nch = nchu;  // no skip segment: every chunk of a unit is a 3x3 chunk
+          if (res) {
+            rres = mkrsrc(p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout);
+#pragma unroll
+            for (int mr = 0; mr < 2; ++mr) {
+              if (resk == 1) {
+                vbu[mr] = vbase(t) + mr * mstep;
+              } else {
+                const int ys = ((t.y0 + wrow) >> 1) + (TW == 16 ? mr : 0);
+                vbu[mr] = (((wimg * p.res_H + ys) * p.res_W + (t.x0 >> 1) + 2 * h) * p.cout + t.ct * XBN + l32) * 4;
+              }
+            }
+          }
+          auto bias_pf = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int nr = 0; nr < 2; ++nr) bias2[nr] = S == 1 ? gld1(p.bias + t.ct * XBN + 32 * nr + l32) : 0.f;
+          };
+          {  // stores: one piece on each of the first 4 chunks; loads: on each of the last 4 (nch >= 8)
+            chunk(I0(), I1(), I0(), I0(), pending, NoLd());
+            chunk(I1(), I1(), I0(), I0(), pending, NoLd());
+            chunk(I2(), I1(), I0(), I0(), pending, NoLd());
+            chunk(I3(), I1(), I0(), I0(), pending, NoLd());
+            for (int k = 4; k < nch - 4; ++k) chunk(I0(), I0(), I0(), I0(), false, NoLd());
+            bias_pf();
+            chunk(I0(), I0(), I0(), I1(), false, Ld());
+            chunk(I0(), I0(), I1(), I1(), false, Ld());
+            chunk(I0(), I0(), I2(), I1(), false, Ld());
+            chunk(I0(), I0(), I3(), I1(), false, Ld());
+          }
+          if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
+            p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
+          // outputs into rv: the epilogue arithmetic of the non-deferred path (x 2^-11, + bias, residual + x)
+#pragma unroll
+          for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+            for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                float x = acc[mr][nr][r] * (1.0f / kLo);  // exact rescale
+                if (S == 1) {
+                  x = x + bias2[nr];
+                  if (res) x = rv[mr][nr][r] + x;  // torch order: x_res + (conv + bias)
+                }
+                rv[mr][nr][r] = x;
+              }
+          if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
+            p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values computed
+          if (X3_ABLATE != 15 && S == 1 && p.gstat) gstats(t, rv);
+          if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0) {
+            p.trace[64 * blockIdx.x + 45] = __builtin_amdgcn_s_memtime();  // statistics done
+            p.trace[64 * blockIdx.x + 63] = __builtin_amdgcn_s_memtime();
+          }
+          pending = true;
+          rdst = S > 1 ? mkrsrc(p.part + ((size_t)z * p.N + t.n0) * img) : mkrsrc(p.out + (size_t)t.n0 * img);
+          vbd = vbase(t);
+          zero();
+        }
+        if (pending) {  // the block's last unit
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) st1(q >> 1, q & 1, r);
+        }
+      };
+      if (S == 1 && p.res && p.res_xform == XF_NONE)
+        run_units(std::integral_constant<int, 1>());
+      else if (S == 1 && p.res)
+        run_units(std::integral_constant<int, 2>());
+      else
+        run_units(std::integral_constant<int, 0>());
+      return;
+    }
+#endif
     for (int u = 0; u < nu; ++u) {
       int z;
       const STile t = unit_of(u, z);
