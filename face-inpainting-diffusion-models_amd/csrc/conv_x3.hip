@@ -37,8 +37,6 @@
 //     s + 2 while chunk s is split and consumed.
 // LDS: A = 4 planes [part hi/lo][channel half h][halo px][8 f16] (<= 21.25 KiB) double-buffered,
 // W = [tap][part][h][64 co][8 f16] (36 KiB) in a 3-slot ring (DMA two chunks ahead).
-#include <type_traits>
-
 #include "conv.h"
 #include "conv_dev.h"
 
@@ -178,11 +176,6 @@ __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int
 
 #ifndef X3_PREF
 #define X3_PREF 2
-#endif
-// X3_DEFER=1: the non-skip instantiations store a unit's outputs during the next unit's chunks and load
-// its residual during its own last chunks (the consumer's deferred epilogue); 0: the round-2 epilogue
-#ifndef X3_DEFER
-#define X3_DEFER 1
 #endif
 #ifndef X3_PINF
 #define X3_PINF 1
@@ -405,14 +398,8 @@ __device__ __forceinline__ f32x16 xmfma(f16x8 a, f16x8 b, f32x16 c) {
 // MFMAs over one staged 3x3 chunk: 9 taps x (3 split products x 2 x 2 fragment blocks);
 // operand = the halo stage (planes of Geo::NP pixels, pb = halo pixel).
 // NPROD = 1 (the f16 precision mode): the hi x hi product only.
-// `extra(tap)` (taps 0-7) issues the deferred epilogue's memory operations between the tap's first MFMA
-// group and its split-product groups, so they drain beside MFMAs instead of in a burst.
-struct XNoExtra {
-  __device__ __forceinline__ void operator()(int) const {}
-};
-template <int TW, int NPROD, typename F = XNoExtra>
-__device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws, const int (&pb)[2],
-                                           F&& extra = F()) {
+template <int TW, int NPROD>
+__device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws, const int (&pb)[2]) {
   using Geo = XGeo<TW>;
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const lds_f* Ah = As + 4 * (h * Geo::NP);
@@ -443,8 +430,6 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
         acc[mr][nr] = xmfma(ah[cur][mr], bs[cur][nr], acc[mr][nr]);
     __builtin_amdgcn_sched_barrier(0);
     if (tap + 1 < 9) fetch(tap + 1, cur ^ 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (tap < 8) extra(tap);
     __builtin_amdgcn_sched_barrier(0);
     if (NPROD == 1) continue;
 #pragma unroll
@@ -554,69 +539,6 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
             }
       }
     };
-    // GroupNorm granule statistics of the unit's output values v[mr][nr][r] (the accumulators after the
-    // epilogue arithmetic, or the deferred epilogue's rv)
-    auto gstats = [&](const STile& t, const auto& v) __attribute__((always_inline)) {
-        // GroupNorm granule statistics of each output channel: over this lane's 32 pixels (two-pass),
-        // then merged with the other column half (lane ^ 32) and over the channel quad (lanes ^ 1,
-        // ^ 2). Every merge joins two equal counts, so Chan's update needs no division:
-        //   mean = ma + d / 2,  M2 = (M2a + M2b) + d^2 n / 2,  d = mb - ma  (n = one side's count)
-        // (bit-identical to gmerge: the factors are powers of two). The partner values come from
-        // v_permlane32_swap and DPP quad permutes (VALU) instead of LDS-routed shuffles, and the two
-        // channel blocks' chains are interleaved.
-        float mean[2], m2[2];
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr) {
-          float sm = 0.f;
-#pragma unroll
-          for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sm += v[mr][nr][r];
-          mean[nr] = sm * (1.0f / 32);
-          float q = 0.f;
-#pragma unroll
-          for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float d = v[mr][nr][r] - mean[nr];
-              q += d * d;
-            }
-          m2[nr] = q;
-        }
-        auto merge = [&](float am, float aq, float bm, float bq, float n, float& om, float& oq) {
-          const float d = bm - am;
-          om = am + d * 0.5f;
-          oq = (aq + bq) + ((d * d) * n) * 0.5f;
-        };
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr) {  // lane ^ 32
-          float ml, mh, ql, qh;
-          wave_halves(mean[nr], ml, mh);
-          wave_halves(m2[nr], ql, qh);
-          merge(ml, ql, mh, qh, 32.f, mean[nr], m2[nr]);
-        }
-        // lanes ^ 1 then ^ 2 within the quad: quad_perm [0,0,2,2] / [1,1,3,3], then [0,1,0,1] / [2,3,2,3]
-#define IFD_QP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false))
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr)
-          merge(IFD_QP(mean[nr], 0xA0), IFD_QP(m2[nr], 0xA0), IFD_QP(mean[nr], 0xF5), IFD_QP(m2[nr], 0xF5), 64.f, mean[nr],
-                m2[nr]);
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr)
-          merge(IFD_QP(mean[nr], 0x44), IFD_QP(m2[nr], 0x44), IFD_QP(mean[nr], 0xEE), IFD_QP(m2[nr], 0xEE), 128.f, mean[nr],
-                m2[nr]);
-#undef IFD_QP
-        if (h == 0 && (l32 & 3) == 0) {
-          const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
-#pragma unroll
-          for (int nr = 0; nr < 2; ++nr) {
-            float* o = p.gstat + (((size_t)(t.n0 + wimg) * (p.cout / 4) + t.ct * 16 + nr * 8 + (l32 >> 2)) *
-                                      p.gstat_E + e) * 2;
-            o[0] = mean[nr];
-            o[1] = m2[nr];
-          }
-        }
-    };
     auto epilogue = [&](const STile& t, int z, bool tstamp = false) {
       if (X3_ABLATE == 13) {  // timing only: no epilogue
         asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
@@ -654,7 +576,67 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           }
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
         p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values + stores issued
-      if (X3_ABLATE != 15 && p.gstat) gstats(t, acc);
+      if (X3_ABLATE != 15 && p.gstat) {
+        // GroupNorm granule statistics of each output channel: over this lane's 32 pixels (two-pass),
+        // then merged with the other column half (lane ^ 32) and over the channel quad (lanes ^ 1,
+        // ^ 2). Every merge joins two equal counts, so Chan's update needs no division:
+        //   mean = ma + d / 2,  M2 = (M2a + M2b) + d^2 n / 2,  d = mb - ma  (n = one side's count)
+        // (bit-identical to gmerge: the factors are powers of two). The partner values come from
+        // v_permlane32_swap and DPP quad permutes (VALU) instead of LDS-routed shuffles, and the two
+        // channel blocks' chains are interleaved.
+        float mean[2], m2[2];
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr) {
+          float sm = 0.f;
+#pragma unroll
+          for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sm += acc[mr][nr][r];
+          mean[nr] = sm * (1.0f / 32);
+          float q = 0.f;
+#pragma unroll
+          for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float d = acc[mr][nr][r] - mean[nr];
+              q += d * d;
+            }
+          m2[nr] = q;
+        }
+        auto merge = [&](float am, float aq, float bm, float bq, float n, float& om, float& oq) {
+          const float d = bm - am;
+          om = am + d * 0.5f;
+          oq = (aq + bq) + ((d * d) * n) * 0.5f;
+        };
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr) {  // lane ^ 32
+          float ml, mh, ql, qh;
+          wave_halves(mean[nr], ml, mh);
+          wave_halves(m2[nr], ql, qh);
+          merge(ml, ql, mh, qh, 32.f, mean[nr], m2[nr]);
+        }
+        // lanes ^ 1 then ^ 2 within the quad: quad_perm [0,0,2,2] / [1,1,3,3], then [0,1,0,1] / [2,3,2,3]
+#define IFD_QP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false))
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+          merge(IFD_QP(mean[nr], 0xA0), IFD_QP(m2[nr], 0xA0), IFD_QP(mean[nr], 0xF5), IFD_QP(m2[nr], 0xF5), 64.f, mean[nr],
+                m2[nr]);
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+          merge(IFD_QP(mean[nr], 0x44), IFD_QP(m2[nr], 0x44), IFD_QP(mean[nr], 0xEE), IFD_QP(m2[nr], 0xEE), 128.f, mean[nr],
+                m2[nr]);
+#undef IFD_QP
+        if (h == 0 && (l32 & 3) == 0) {
+          const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
+#pragma unroll
+          for (int nr = 0; nr < 2; ++nr) {
+            float* o = p.gstat + (((size_t)(t.n0 + wimg) * (p.cout / 4) + t.ct * 16 + nr * 8 + (l32 >> 2)) *
+                                      p.gstat_E + e) * 2;
+            o[0] = mean[nr];
+            o[1] = m2[nr];
+          }
+        }
+      }
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
         p.trace[64 * blockIdx.x + 45] = __builtin_amdgcn_s_memtime();  // statistics done
     };
@@ -759,155 +741,6 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     zero();
     XBARRIER_CONSUMER();  // chunk 0 staged
     int j = 0;  // position in the block's chunk stream: ring slot j % 3, A stage j & 1
-#if X3_DEFER
-    if (!SKIP && nchu >= 8) {
-      // Deferred epilogue (the non-skip instantiations whose units have >= 8 chunks; shorter units - the
-      // split-K and 8x8 layers, the input conv - keep the epilogue below: two phases of rv that overlap
-      // in one chunk would not fit the register budget). A unit's outputs (x 2^-11, bias, residual) are
-      // computed into rv at the unit's end - with its GroupNorm granule statistics - and STORED during
-      // the next unit's first chunks, two registers per tap between MFMA groups; the residual of a unit
-      // is LOADED into rv the same way during its last chunks. IFD_TRACE stamps (round 2, the 128-channel
-      // 256^2 layers) had the 64 dword stores per wave at ~3.4k cycles of a ~10k-cycle unit transition
-      // and the residual's 64 loads, issued in one burst, at +3.7k on their chunk: the CU's
-      // vector-memory issue rate, not the bytes. rv is the register set the epilogue already used.
-      const size_t img = (size_t)p.H * p.W * p.cout;
-      bool pending = false;  // rv holds the previous unit's outputs, not yet stored
-      rsrc_t rdst = mkrsrc(p.out), rres = mkrsrc(p.out);
-      int vbd = 0;
-      // XF_UP residual offsets, separable like roff: register (mr, r) of lane (h, l32) sits at output
-      // row wrow + (32 / TW) mr (+ (r >> 3) at TW = 16) and column 4 h + c(r), c(r) = (8 (r >> 2) + (r & 3))
-      // mod TW (4 h + c(r) < TW); tile origins are even, so the source pixel is row (y0 + wrow) / 2 + mr
-      // (TW = 16) or (y0 + wrow) / 2 (TW = 32), column x0 / 2 + 2 h + c(r) / 2
-      int vbu[2] = {0, 0};
-      auto uoff = [&](int r) { return (((8 * (r >> 2) + (r & 3)) & (TW - 1)) >> 1) * p.cout * 4; };
-      auto st1 = [&](int mr, int nr, int r) __attribute__((always_inline)) {
-        if (X3_ABLATE != 14)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rv[mr][nr][r]), rdst,
-                                                vbd + mr * mstep + nr * 128, roff(r), 0);
-      };
-      auto ld1 = [&](auto UP, int mr, int nr, int r) __attribute__((always_inline)) {
-        if (!decltype(UP)::value) {
-          rv[mr][nr][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rres, vbu[mr] + nr * 128, roff(r), 0));
-        } else {  // XF_UP: nearest-upsampled residual, lane part vbu[mr] + wave-uniform part uoff(r)
-          rv[mr][nr][r] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(rres, vbu[mr] + nr * 128, uoff(r), 0));
-        }
-      };
-      // one chunk whose taps 0-7 also store pieces [QS, QS + NS) and load pieces [QL, QL + NL) of rv
-      // (piece q = block (q >> 1, q & 1), 16 registers, two per tap); LD is compile-time so that rv has
-      // one definition point per path (a merge of a loaded and an unloaded copy would cost a vmcnt wait)
-      auto chunk = [&](auto QS, auto NS, auto QL, auto NL, bool do_st, auto LD) __attribute__((always_inline)) {
-        constexpr int qs = decltype(QS)::value, ns = decltype(NS)::value;
-        constexpr int ql = decltype(QL)::value, nl = decltype(NL)::value;
-        constexpr int ld = decltype(LD)::value;  // 0 no loads, 1 identity residual, 2 nearest-up residual
-        auto extra = [&](int tap) __attribute__((always_inline)) {
-          if (ns > 0 && do_st) {
-#pragma unroll
-            for (int q = qs; q < qs + ns; ++q) {
-              st1(q >> 1, q & 1, 2 * tap);
-              st1(q >> 1, q & 1, 2 * tap + 1);
-            }
-          }
-          if (ld) {
-            using Up = std::integral_constant<bool, ld == 2>;
-#pragma unroll
-            for (int q = ql; q < ql + nl; ++q) {
-              ld1(Up(), q >> 1, q & 1, 2 * tap);
-              ld1(Up(), q >> 1, q & 1, 2 * tap + 1);
-            }
-          }
-        };
-        stamp(j);
-        if (X3_ABLATE != 4) consume_x3<TW, NPROD>(acc, A0 + (j & 1) * XA, W0 + (j % 3) * XW, pb, extra);
-        stamp(j, 16);
-        ++j;
-        XBARRIER_CONSUMER();
-      };
-      using I0 = std::integral_constant<int, 0>;
-      using I1 = std::integral_constant<int, 1>;
-      using I2 = std::integral_constant<int, 2>;
-      using I3 = std::integral_constant<int, 3>;
-      using NoLd = std::integral_constant<int, 0>;
-      auto run_units = [&](auto RES) __attribute__((always_inline)) {
-        constexpr int resk = decltype(RES)::value;  // S == 1 and a residual: 1 identity, 2 nearest-up
-        constexpr bool res = resk != 0;
-        using Ld = std::integral_constant<int, resk>;
-        for (int u = 0; u < nu; ++u) {
-          int z;
-          const STile t = unit_of(u, z);
-          const int nch = nchu;  // no skip segment: every chunk of a unit is a 3x3 chunk
-          if (res) {
-            rres = mkrsrc(p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout);
-#pragma unroll
-            for (int mr = 0; mr < 2; ++mr) {
-              if (resk == 1) {
-                vbu[mr] = vbase(t) + mr * mstep;
-              } else {
-                const int ys = ((t.y0 + wrow) >> 1) + (TW == 16 ? mr : 0);
-                vbu[mr] = (((wimg * p.res_H + ys) * p.res_W + (t.x0 >> 1) + 2 * h) * p.cout + t.ct * XBN + l32) * 4;
-              }
-            }
-          }
-          auto bias_pf = [&]() __attribute__((always_inline)) {
-#pragma unroll
-            for (int nr = 0; nr < 2; ++nr) bias2[nr] = S == 1 ? gld1(p.bias + t.ct * XBN + 32 * nr + l32) : 0.f;
-          };
-          {  // stores: one piece on each of the first 4 chunks; loads: on each of the last 4 (nch >= 8)
-            chunk(I0(), I1(), I0(), I0(), pending, NoLd());
-            chunk(I1(), I1(), I0(), I0(), pending, NoLd());
-            chunk(I2(), I1(), I0(), I0(), pending, NoLd());
-            chunk(I3(), I1(), I0(), I0(), pending, NoLd());
-            for (int k = 4; k < nch - 4; ++k) chunk(I0(), I0(), I0(), I0(), false, NoLd());
-            bias_pf();
-            chunk(I0(), I0(), I0(), I1(), false, Ld());
-            chunk(I0(), I0(), I1(), I1(), false, Ld());
-            chunk(I0(), I0(), I2(), I1(), false, Ld());
-            chunk(I0(), I0(), I3(), I1(), false, Ld());
-          }
-          if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
-            p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
-          // outputs into rv: the epilogue arithmetic of the non-deferred path (x 2^-11, + bias, residual + x)
-#pragma unroll
-          for (int nr = 0; nr < 2; ++nr)
-#pragma unroll
-            for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                float x = acc[mr][nr][r] * (1.0f / kLo);  // exact rescale
-                if (S == 1) {
-                  x = x + bias2[nr];
-                  if (res) x = rv[mr][nr][r] + x;  // torch order: x_res + (conv + bias)
-                }
-                rv[mr][nr][r] = x;
-              }
-          if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
-            p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values computed
-          if (X3_ABLATE != 15 && S == 1 && p.gstat) gstats(t, rv);
-          if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0) {
-            p.trace[64 * blockIdx.x + 45] = __builtin_amdgcn_s_memtime();  // statistics done
-            p.trace[64 * blockIdx.x + 63] = __builtin_amdgcn_s_memtime();
-          }
-          pending = true;
-          rdst = S > 1 ? mkrsrc(p.part + ((size_t)z * p.N + t.n0) * img) : mkrsrc(p.out + (size_t)t.n0 * img);
-          vbd = vbase(t);
-          zero();
-        }
-        if (pending) {  // the block's last unit
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) st1(q >> 1, q & 1, r);
-        }
-      };
-      if (S == 1 && p.res && p.res_xform == XF_NONE)
-        run_units(std::integral_constant<int, 1>());
-      else if (S == 1 && p.res)
-        run_units(std::integral_constant<int, 2>());
-      else
-        run_units(std::integral_constant<int, 0>());
-      return;
-    }
-#endif
     for (int u = 0; u < nu; ++u) {
       int z;
       const STile t = unit_of(u, z);
