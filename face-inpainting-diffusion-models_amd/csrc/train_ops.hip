@@ -8,6 +8,7 @@
 // (the modules differentiated). Activations are NHWC fp32; weights live in the reference's
 // torch layouts inside one flat parameter buffer (ifd/train.py) and are packed per step.
 // Every reduction runs in a fixed order (no atomics): a step is bit-reproducible.
+#include <type_traits>
 #include "../../include/ifd_train.h"
 
 #include <cmath>
@@ -332,8 +333,6 @@ constexpr int WX_PX = 64;                 // output pixels per chunk
 constexpr int WX_HMAX = 136;              // halo pixels: 4 x 34, 6 x 18, 10 x 10
 constexpr int WX_D = 2 * WX_PX * 64;      // f16 per stage: dY, both parts
 constexpr int WX_X = 2 * WX_HMAX * 64;    // X halo, both parts
-constexpr int WX_DI = WX_PX * 16 / 256;   // dY 16-B items per thread (4)
-constexpr int WX_XI = (WX_HMAX * 16 + 255) / 256;  // X halo items per thread (9)
 typedef _Float16 wx_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 wx_h4 __attribute__((ext_vector_type(4)));
 typedef unsigned wx_u2 __attribute__((ext_vector_type(2)));
@@ -347,22 +346,38 @@ __device__ __forceinline__ wx_h4 wx_tr(const _Float16* L, int off) {
   return __builtin_bit_cast(wx_h4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) wx_hv4*)(L + off)));
 }
 
+// Threads per block: the 3x3 kernel runs 8 waves, two per SIMD - waves w and w + 4 own the same 32 x 32
+// quadrant, taps 0-4 and 5-8 (80 / 64 accumulator registers instead of 144), so while one waits on an LDS
+// read or its staging the other's MFMAs run (round 2: one wave per SIMD with all 9 taps, ~45 % of its
+// MFMA-bound time); the 1x1 kernel keeps 4 waves.
+template <int TAPS>
+struct WxCfg {
+  static constexpr int NT = TAPS == 9 ? 512 : 256;
+  static constexpr int DI = WX_PX * 16 / NT;                   // dY 16-B items per thread
+  static constexpr int XI = (WX_HMAX * 16 + NT - 1) / NT;      // X halo items per thread
+  static constexpr int NG = TAPS == 9 ? 2 : 1;                 // tap groups
+  static constexpr int NTMAX = TAPS == 9 ? 5 : 1;              // accumulators per wave
+};
+
 // colpart (optional): the bias gradient's column sums of dY, fused: the ci-tile-0 blocks add their
-// split's pixels per channel (fixed order: per thread over chunks, then the 16 pixel lanes in lane
+// split's pixels per channel (fixed order: per thread over chunks, then the pixel lanes in lane
 // order) into colpart[split][cout]; colsum_final_kernel adds the splits in order.
 // TAPS = 9 (3x3, halo of one pixel) or 1 (1x1: the chunk's own pixels, no halo).
 template <int TAPS>
-__global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
+__global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
+  using Cf = WxCfg<TAPS>;
+  constexpr int NT = Cf::NT, WX_DI = Cf::DI, WX_XI = Cf::XI, NTMAX = Cf::NTMAX;
   constexpr int HALO = TAPS == 9 ? 1 : 0;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
-  __shared__ f32x4 csred[256];
+  __shared__ f32x4 csred[NT];
   const int cin = a.c0;
   const int nci = (cin + 63) / 64;
   const int cit = blockIdx.x % nci, cot = blockIdx.x / nci;
   const int co0 = cot * 64, ci0 = cit * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5;
-  const int wr = 32 * (wave & 1), wc = 32 * (wave >> 1);
+  const int quad = wave & 3, grp = Cf::NG > 1 ? wave >> 2 : 0;  // quadrant; tap group (taps 0-4 / 5-8)
+  const int wr = 32 * (quad & 1), wc = 32 * (quad >> 1);
   const int Wc = a.W < 32 ? a.W : 32, R = WX_PX / Wc;
   const int HWc = Wc + 2 * HALO, HP = (R + 2 * HALO) * HWc;
   const int lwc = __builtin_ctz(Wc);
@@ -370,23 +385,23 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
   const int64_t nch = (int64_t)a.N * rows_per_img * segs;
   const int64_t c_beg = (int64_t)blockIdx.y * a.chunks_per_split;
   const int64_t c_end = c_beg + a.chunks_per_split < nch ? c_beg + a.chunks_per_split : nch;
-  f32x16 acc[TAPS];
+  f32x16 acc[NTMAX];
 #pragma unroll
-  for (int t = 0; t < TAPS; ++t)
+  for (int t = 0; t < NTMAX; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   float gmax = 0.f;
   const bool do_cs = colpart && cit == 0;
   f32x4 csum = {0.f, 0.f, 0.f, 0.f};
   if (c_beg < c_end) {
-    // staging items: (pixel i >> 4, channel quad i & 15), i = tid + 256 k; quad fixed per thread
+    // staging items: (pixel i >> 4, channel quad i & 15), i = tid + NT k; quad fixed per thread
     const int cq = tid & 15;
     const bool co_ok = co0 + 4 * cq + 3 < a.cout, ci_ok = ci0 + 4 * cq + 3 < cin;
     f32x4 dv[WX_DI], xv[WX_XI];
     int xhy[WX_XI], xhx[WX_XI];
 #pragma unroll
     for (int k = 0; k < WX_XI; ++k) {
-      const int hp = (tid + 256 * k) >> 4;
+      const int hp = (tid + NT * k) >> 4;
       xhy[k] = hp < HP ? hp / HWc - HALO : -1000000;  // halo row / column relative to the chunk origin
       xhx[k] = hp % HWc - HALO;
     }
@@ -404,7 +419,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
       const int64_t img = (int64_t)n * a.H;
 #pragma unroll
       for (int k = 0; k < WX_DI; ++k) {
-        const int m = (tid + 256 * k) >> 4;
+        const int m = (tid + NT * k) >> 4;
         const int64_t pix = (img + y0 + (m >> lwc)) * a.W + x0 + (m & (Wc - 1));
         dv[k] = co_ok ? *reinterpret_cast<const f32x4*>(a.dy + pix * a.cout + co0 + 4 * cq) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -427,7 +442,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
         const bool isd = it < WX_DI;
         const int k = isd ? it : it - WX_DI;
         const f32x4 v = isd ? dv[k] : xv[k];
-        const int row = isd ? (tid + 256 * k) >> 4 : (tid + 256 * k) >> 4;
+        const int row = (tid + NT * k) >> 4;
         if (!isd && row >= HP) continue;
         if (isd && do_cs) csum += v;
         wx_h4 hi, lo;
@@ -454,6 +469,78 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
     // which 8 of the k-step's 16 pixels); lane 4q + p of the group addresses row q, columns 4p .. 4p + 3
     const int G = lane >> 4, q = (lane & 15) >> 2, pcol = 4 * (lane & 3);
     const int cA = wr + 16 * (G & 1) + pcol, cB = wc + 16 * (G & 1) + pcol;
+    // MFMAs of one staged chunk for taps T0 .. T0 + NTAP - 1 into acc[0 .. NTAP - 1] (compile-time, so the
+    // accumulators stay registers; the two tap groups are two copies of this code, selected per wave)
+    auto mfma_chunk = [&](auto T0c, auto NTc, const _Float16* L, _Float16* Ln, bool nxt) __attribute__((always_inline)) {
+      constexpr int T0 = decltype(T0c)::value, NTAP = decltype(NTc)::value;
+      // the lane's row / column roles laundered per chunk: the fragment addresses are then computed next
+      // to their reads instead of ~80 of them being hoisted out of the chunk loop into registers (the
+      // round-2 kernel held 392 VGPRs at one wave per SIMD; two waves per SIMD leave 256 each)
+      int cAl = cA, cBl = cB, ql = q, hl = h;
+      asm volatile("" : "+v"(cAl), "+v"(cBl), "+v"(ql), "+v"(hl));
+      const _Float16* Dh = L;
+      const _Float16* Dl = L + WX_PX * 64;
+      const _Float16* Xh = L + WX_D;
+      const _Float16* Xl = Xh + WX_HMAX * 64;
+      // Software-pipelined: taps in pairs whose MFMAs alternate (no back-to-back accumulator
+      // dependence), the next pair's B fragments read after the current pair's first MFMAs, the
+      // next k-step's A fragments during the last pair (a read the MFMA waits on costs its latency).
+      auto fetchA = [&](int st, wx_h8& ahi, wx_h8& alo) {
+        const int m0 = 16 * st + 8 * hl;
+        const int oa0 = wx_off(m0 + ql, cAl), oa1 = wx_off(m0 + 4 + ql, cAl);
+        const wx_h4 ah0 = wx_tr(Dh, oa0), ah1 = wx_tr(Dh, oa1), al0 = wx_tr(Dl, oa0), al1 = wx_tr(Dl, oa1);
+        ahi = wx_h8{ah0[0], ah0[1], ah0[2], ah0[3], ah1[0], ah1[1], ah1[2], ah1[3]};
+        alo = wx_h8{al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
+      };
+      auto fetchB = [&](int st, int t, wx_h8& bhi, wx_h8& blo) {
+        const int m0 = 16 * st + 8 * hl;  // this lane-half's 8 pixels of the k-step: one row segment
+        const int hb = (m0 >> lwc) * HWc + (m0 & (Wc - 1));
+        const int r0 = TAPS == 9 ? hb + (t / 3) * HWc + (t % 3) : hb;
+        const int ob0 = wx_off(r0 + ql, cBl), ob1 = wx_off(r0 + 4 + ql, cBl);
+        const wx_h4 bh0 = wx_tr(Xh, ob0), bh1 = wx_tr(Xh, ob1), bl0 = wx_tr(Xl, ob0), bl1 = wx_tr(Xl, ob1);
+        bhi = wx_h8{bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
+        blo = wx_h8{bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
+      };
+      constexpr int NST = WX_PX / 16, NPAIR = (NTAP + 1) / 2;
+      wx_h8 ahi, alo, b0h, b0l, b1h, b1l;
+      fetchA(0, ahi, alo);
+      fetchB(0, T0, b0h, b0l);
+      if (NTAP > 1) fetchB(0, T0 + 1, b1h, b1l);
+#pragma unroll
+      for (int st = 0; st < NST; ++st) {
+#pragma unroll
+        for (int pp = 0; pp < NPAIR; ++pp) {
+          const int l0 = 2 * pp, l1 = 2 * pp + 1;  // local tap indices (accumulators)
+          const bool two = l1 < NTAP;
+          acc[l0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b0h, acc[l0], 0, 0, 0);
+          if (two) acc[l1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b1h, acc[l1], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          // next pair (or the next k-step's first pair, and its A fragments)
+          wx_h8 n0h, n0l, n1h, n1l, nah, nal;
+          const bool last = pp + 1 == NPAIR;
+          const int nst = last ? st + 1 : st, nl0 = last ? 0 : l0 + 2;
+          const bool more = nst < NST;
+          if (more) {
+            fetchB(nst, T0 + nl0, n0h, n0l);
+            if (nl0 + 1 < NTAP) fetchB(nst, T0 + nl0 + 1, n1h, n1l);
+            if (last) fetchA(nst, nah, nal);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          acc[l0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b0l, acc[l0], 0, 0, 0);
+          if (two) acc[l1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b1l, acc[l1], 0, 0, 0);
+          acc[l0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b0h, acc[l0], 0, 0, 0);
+          if (two) acc[l1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b1h, acc[l1], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (more) {
+            b0h = n0h; b0l = n0l;
+            if (nl0 + 1 < NTAP) { b1h = n1h; b1l = n1l; }
+            if (last) { ahi = nah; alo = nal; }
+          }
+        }
+        if (nxt) store_part(Ln, st);  // (block-uniform)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
     // prologue: chunk c_beg staged, chunk c_beg + 1 in flight. Iteration c: MFMAs of chunk c from
     // lds[c & 1] with chunk c + 1's staging slices between its k-steps into lds[(c + 1) & 1] (read by
     // chunk c - 1, whose MFMAs every wave finished before the previous barrier), then chunk c + 2's loads
@@ -466,68 +553,10 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
       _Float16* L = lds[c & 1];
       _Float16* Ln = lds[(c + 1) & 1];
       const bool nxt = c + 1 < c_end;
-      const _Float16* Dh = L;
-      const _Float16* Dl = L + WX_PX * 64;
-      const _Float16* Xh = L + WX_D;
-      const _Float16* Xl = Xh + WX_HMAX * 64;
-      // Software-pipelined: taps in pairs whose MFMAs alternate (no back-to-back accumulator
-      // dependence), the next pair's B fragments read after the current pair's first MFMAs, the
-      // next k-step's A fragments during the last pair (a read the MFMA waits on costs its latency).
-      auto fetchA = [&](int st, wx_h8& ahi, wx_h8& alo) {
-        const int m0 = 16 * st + 8 * h;
-        const int oa0 = wx_off(m0 + q, cA), oa1 = wx_off(m0 + 4 + q, cA);
-        const wx_h4 ah0 = wx_tr(Dh, oa0), ah1 = wx_tr(Dh, oa1), al0 = wx_tr(Dl, oa0), al1 = wx_tr(Dl, oa1);
-        ahi = wx_h8{ah0[0], ah0[1], ah0[2], ah0[3], ah1[0], ah1[1], ah1[2], ah1[3]};
-        alo = wx_h8{al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
-      };
-      auto fetchB = [&](int st, int t, wx_h8& bhi, wx_h8& blo) {
-        const int m0 = 16 * st + 8 * h;  // this lane-half's 8 pixels of the k-step: one row segment
-        const int hb = (m0 >> lwc) * HWc + (m0 & (Wc - 1));
-        const int r0 = TAPS == 9 ? hb + (t / 3) * HWc + (t % 3) : hb;
-        const int ob0 = wx_off(r0 + q, cB), ob1 = wx_off(r0 + 4 + q, cB);
-        const wx_h4 bh0 = wx_tr(Xh, ob0), bh1 = wx_tr(Xh, ob1), bl0 = wx_tr(Xl, ob0), bl1 = wx_tr(Xl, ob1);
-        bhi = wx_h8{bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
-        blo = wx_h8{bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
-      };
-      constexpr int NST = WX_PX / 16, NPAIR = (TAPS + 1) / 2;
-      wx_h8 ahi, alo, b0h, b0l, b1h, b1l;
-      fetchA(0, ahi, alo);
-      fetchB(0, 0, b0h, b0l);
-      if (TAPS > 1) fetchB(0, 1, b1h, b1l);
-#pragma unroll
-      for (int st = 0; st < NST; ++st) {
-#pragma unroll
-        for (int pp = 0; pp < NPAIR; ++pp) {
-          const int t0 = 2 * pp, t1 = 2 * pp + 1;
-          const bool two = t1 < TAPS;
-          acc[t0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b0h, acc[t0], 0, 0, 0);
-          if (two) acc[t1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b1h, acc[t1], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          // next pair (or the next k-step's first pair, and its A fragments)
-          wx_h8 n0h, n0l, n1h, n1l, nah, nal;
-          const bool last = pp + 1 == NPAIR;
-          const int nst = last ? st + 1 : st, nt0 = last ? 0 : t0 + 2;
-          const bool more = nst < NST;
-          if (more) {
-            fetchB(nst, nt0, n0h, n0l);
-            if (nt0 + 1 < TAPS) fetchB(nst, nt0 + 1, n1h, n1l);
-            if (last) fetchA(nst, nah, nal);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          acc[t0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b0l, acc[t0], 0, 0, 0);
-          if (two) acc[t1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b1l, acc[t1], 0, 0, 0);
-          acc[t0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b0h, acc[t0], 0, 0, 0);
-          if (two) acc[t1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b1h, acc[t1], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          if (more) {
-            b0h = n0h; b0l = n0l;
-            if (nt0 + 1 < TAPS) { b1h = n1h; b1l = n1l; }
-            if (last) { ahi = nah; alo = nal; }
-          }
-        }
-        if (nxt) store_part(Ln, st);  // (block-uniform)
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      if (TAPS == 9 && grp == 1)
+        mfma_chunk(std::integral_constant<int, 5>(), std::integral_constant<int, 4>(), L, Ln, nxt);
+      else
+        mfma_chunk(std::integral_constant<int, 0>(), std::integral_constant<int, TAPS == 9 ? 5 : 1>(), L, Ln, nxt);
       if (c + 2 < c_end) load(c + 2);
       __syncthreads();
     }
@@ -538,7 +567,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
     __syncthreads();
     if (tid < 16) {
       f32x4 t = csred[tid];
-      for (int r = 1; r < 16; ++r) t += csred[tid + 16 * r];
+      for (int r = 1; r < NT / 16; ++r) t += csred[tid + 16 * r];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int co = co0 + 4 * tid + j;
@@ -549,13 +578,16 @@ __global__ __launch_bounds__(256, 1) void wgrad_x3_kernel(WgArgs a, unsigned* gu
   // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin][TAPS]
   float* slab = a.part + (size_t)blockIdx.y * a.cout * cin * TAPS;
   const int ci = ci0 + wc + (lane & 31);
+  const int tbase = TAPS == 9 ? 5 * grp : 0, ntap = TAPS == 9 ? (grp ? 4 : 5) : 1;
 #pragma unroll
-  for (int t = 0; t < TAPS; ++t)
+  for (int lt = 0; lt < NTMAX; ++lt) {
+    if (lt >= ntap) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + wr + 8 * (r >> 2) + 4 * h + (r & 3);
-      if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * TAPS + t] = acc[t][r];
+      if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * TAPS + tbase + lt] = acc[lt][r];
     }
+  }
 }
 
 __global__ void slab_reduce_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out,
@@ -1789,9 +1821,11 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   // bias gradient fused into the kernel when the column-sum workspace holds one row per split
   const bool fused_db = db && colpart && (int64_t)S * cout <= colpart_floats && cout % 4 == 0;
   if (taps == 9)
-    hipLaunchKernelGGL(wgrad_x3_kernel<9>, dim3(tiles, S), dim3(256), 0, s, a, guard, fused_db ? colpart : nullptr);
+    hipLaunchKernelGGL(wgrad_x3_kernel<9>, dim3(tiles, S), dim3(WxCfg<9>::NT), 0, s, a, guard,
+                       fused_db ? colpart : nullptr);
   else
-    hipLaunchKernelGGL(wgrad_x3_kernel<1>, dim3(tiles, S), dim3(256), 0, s, a, guard, fused_db ? colpart : nullptr);
+    hipLaunchKernelGGL(wgrad_x3_kernel<1>, dim3(tiles, S), dim3(WxCfg<1>::NT), 0, s, a, guard,
+                       fused_db ? colpart : nullptr);
   const int64_t n = (int64_t)cout * c0 * taps;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (fused_db) {
