@@ -177,10 +177,6 @@ __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int
 #ifndef X3_PREF
 #define X3_PREF 2
 #endif
-// X3_SETS3=1: the non-skip instantiations load the halo three chunks ahead (three register sets)
-#ifndef X3_SETS3
-#define X3_SETS3 1
-#endif
 #ifndef X3_PINF
 #define X3_PINF 1
 #endif
@@ -876,72 +872,6 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         XBARRIER_PRODUCER(2);
     }
   };
-#if X3_SETS3
-  if constexpr (!SKIP) {
-    // Non-skip instantiations: halo loads THREE chunks ahead (a third register set; the producers use
-    // ~110 of the kernel's 255 VGPRs), the weight DMA still two ahead (3-slot ring). Interval j: LDS
-    // writes of chunk j+1 (its loads issued two intervals ago), DMA of chunk j+2, halo loads of chunk
-    // j+3, barrier once chunk j+1's DMA (interval j-1) has landed - younger are chunk j+2's loads, chunk
-    // j+2's DMA and chunk j+3's loads: the two-set literal (29 / 33). Two cursors, one per stream.
-    typename XProducer<XF, SKIP, TW, NPROD>::Set s2;
-    int jd = 0, ud = 0, kd = 0, zd = 0;
-    STile td = unit_of(0, zd);
-    auto dma_next = [&]() {
-      const int c = __builtin_amdgcn_readfirstlane(zd * nchu + kd);
-      P.dma(p, td.ct, true, c, nmain, nskip, W0 + (jd % 3) * XW);
-      if (jd + 1 < J) {
-        ++jd;
-        if (++kd == nchu) {
-          kd = 0;
-          td = unit_of(++ud, zd);
-        }
-      } else {
-        jd += 3;  // clamped repeats keep writing slot (J - 1) % 3 (identical bytes)
-      }
-    };
-    auto load_next = [&](typename XProducer<XF, SKIP, TW, NPROD>::Set& st) {
-      const int c = __builtin_amdgcn_readfirstlane(zl * nchu + kl);
-      P.enter(p, tl, ul);
-      P.load(st, p, true, c);
-      if (jl + 1 < J) {  // past the end: re-load the last chunk (fixed op counts)
-        ++jl;
-        if (++kl == nchu) {
-          kl = 0;
-          tl = unit_of(++ul, zl);
-        }
-      }
-    };
-    dma_next();      // chunk 0
-    load_next(s0);
-    dma_next();      // chunk 1
-    load_next(s1);
-    load_next(s2);   // chunk 2's loads
-    P.store(s0, p.act, A0);
-    // chunk 0's DMA landed: younger are its loads, chunk 1's DMA and loads, chunk 2's loads
-    if constexpr (Geo::LOADS == 10)
-      XBARRIER_PRODUCER(39);
-    else
-      XBARRIER_PRODUCER(45);
-    for (int j = 0; j < J; j += 3) {
-      if (j + 1 < J) P.store(s1, p.act, A0 + ((j + 1) & 1) * XA);
-      dma_next();      // chunk j+2
-      load_next(s0);   // chunk j+3
-      barrier();
-      if (j + 1 >= J) break;
-      if (j + 2 < J) P.store(s2, p.act, A0 + (j & 1) * XA);
-      dma_next();      // chunk j+3
-      load_next(s1);   // chunk j+4
-      barrier();
-      if (j + 2 >= J) break;
-      if (j + 3 < J) P.store(s0, p.act, A0 + ((j + 1) & 1) * XA);
-      dma_next();      // chunk j+4
-      load_next(s2);   // chunk j+5
-      barrier();
-    }
-    if (p.guard && P.gmax >= 65504.0f) atomicOr(p.guard, 1u);
-    return;
-  }
-#endif
   issue(s0);  // chunk 0
   const int main0 = lastmain;
   issue(s1);  // chunk 1
