@@ -107,6 +107,29 @@ int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t str
 // 3xf16 split-precision streaming kernel (conv_x3.hip); wpack = the x3 packing (pack_conv_x3).
 bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn);
 int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream);
+// Wide-unit variant (conv_x3w.hip): 8 x 16 pixels x 128 output channels per unit, weights from L2
+// straight into the MFMA waves' registers; wpack = pack_conv_x3 with BN = 128.
+void conv_x3w_geometry(ConvParams& p, int H, int W, int N);
+bool conv_x3w_eligible(const ConvParams& p, int taps, int xform);
+int launch_conv_x3w(const ConvParams& p, int xform, hipStream_t stream);
+
+// A ResBlock's 1x1 skip_connection on split f16 MFMAs as its own launch (skip_x3.hip):
+// out = bias + W * cat(s0, s1) per pixel, NHWC fp32 in and out; conv2 then adds it as its residual.
+struct Skip1x1Params {
+  const float* s0; int sc0;
+  const float* s1; int sc1;
+  int npix;           // N * H * W (a multiple of 32)
+  int cout;
+  const void* wpack;  // pack_skip1x1_x3 (unet.hip): [cout/ntc][K/16][part][h][ntc][8] f16
+  const float* bias;  // [cout] (the skip bias only)
+  float* out;         // [npix][cout]
+  unsigned* guard;    // range guard word (ConvParams::guard)
+  int ntc;            // output channels per block, skip_x3_ntc(K, cout)
+  int nprod;          // 3 (3xf16) or 1 (f16)
+};
+int skip_x3_ntc(int K, int cout);  // 128, 64 or 32 (the tile's split weights fit 128 KiB of LDS); 0 if none
+bool skip_x3_eligible(const Skip1x1Params& p);
+int launch_skip_x3(const Skip1x1Params& p, hipStream_t stream);
 
 // fp32 output-head conv (conv_head.hip): 3x3, cout 6 or 3, NCHW / sampler-step epilogues.
 bool conv_head_eligible(const ConvParams& p, int taps, int xform);

@@ -21,6 +21,12 @@ struct ConvW {
   size_t head_off = 0;  // float offset of the output-head packing (conv_head.hip), 0 if none
   size_t head_x3_off = 0;  // the 3xf16 head's split packing (conv_head_x3_pack), 0 if none
   bool head_x3_ok = false;  // every head weight within the split's range
+  // the skip segment as its own launch (skip_x3.hip) in the split modes: split 1x1 packing, the
+  // conv's own bias and the skip bias apart (b_off holds their sum for the fused kernels)
+  size_t sk_off = 0, bmain_off = 0, sbias_off = 0;
+  size_t x3w_off = 0;  // the split packing at BN = 128 for the wide-unit kernel (conv_x3w.hip), 0 if none
+  int sk_ntc = 0;
+  bool sk_ok = false;
   std::string wname, bname, swname, sbname;  // source parameter names
 };
 
@@ -36,6 +42,7 @@ struct ResP {
   int xf = XF_NONE;
   GNW gn1, gn2;
   ConvW conv1, conv2;
+  ConvW conv2_res;  // conv2 without its skip segment (bias = conv2's own): the separate-skip plan
   int emb_off = 0;
 };
 
@@ -170,6 +177,8 @@ class Model {
   int opt_lds_pad_ = 0;     // extra LDS bytes per fp32 conv block
   int opt_invariant_ = 0;   // batch-invariant geometry (results independent of the batch split)
   int opt_x3_order_ = 0;    // split kernel unit order (ConvParams::opt_x3_order)
+  int opt_x3w_ = 64;        // split modes: wide-unit 3x3 kernel at resolutions >= this (0 off)
+  int opt_skip_sep_ = 64;   // split modes: ResBlock skip_connection as its own launch at resolutions >= this (0 off)
   void fill_opts(ConvParams& p) const {
     p.opt_x3_order = opt_x3_order_;
     p.opt_bm128 = opt_bm128_;

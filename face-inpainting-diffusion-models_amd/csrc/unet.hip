@@ -33,6 +33,8 @@ Model::Model(const ifd_config& cfg) : cfg_(cfg) {
   opt_lds_pad_ = env_int("IFD_CONV_LDS_PAD", 0);
   opt_invariant_ = env_int("IFD_BATCH_INVARIANT", 0) != 0;
   opt_x3_order_ = env_int("IFD_X3_ORDER", 0);
+  opt_skip_sep_ = env_int("IFD_SKIP_SEP", 64);
+  opt_x3w_ = env_int("IFD_X3W", 64);
 }
 
 int Model::set_option(const std::string& key, int v) {
@@ -54,6 +56,12 @@ int Model::set_option(const std::string& key, int v) {
   } else if (key == "x3_order") {
     IFD_REQUIRE(v >= 0 && v <= 2, "x3_order must be 0, 1 or 2");
     opt_x3_order_ = v;
+  } else if (key == "x3w") {
+    IFD_REQUIRE(v >= 0, "x3w must be >= 0");
+    opt_x3w_ = v;
+  } else if (key == "skip_sep") {
+    IFD_REQUIRE(v >= 0, "skip_sep must be >= 0");
+    opt_skip_sep_ = v;
   } else if (key == "batch_invariant") {
     if ((v != 0) != (opt_invariant_ != 0)) ws_B_ = 0;  // split-K slab sizing depends on it: re-plan
     opt_invariant_ = v != 0;
@@ -72,6 +80,8 @@ int Model::get_option(const std::string& key, int* v) const {
   else if (key == "lds_pad") *v = opt_lds_pad_;
   else if (key == "batch_invariant") *v = opt_invariant_;
   else if (key == "x3_order") *v = opt_x3_order_;
+  else if (key == "skip_sep") *v = opt_skip_sep_;
+  else if (key == "x3w") *v = opt_x3w_;
   else IFD_REQUIRE(false, "unknown option " + key);
   return 0;
 }
@@ -410,6 +420,36 @@ static bool pack_skip_x3(const std::vector<float>& w, int cout, int cin, int bn,
   return ok;
 }
 
+// Split packing of a skip_connection for skip_x3.hip: [cout/ntc][K/16][part][h][ntc][8] f16, element
+// (part, h, col, j) of (tile nt, step ks) = split part of Ws[nt*ntc + col][16 ks + 8 h + j] (the MFMA
+// B operand of lane (h, col)). Same parts and range check as pack_conv_x3.
+static bool pack_skip1x1_x3(const std::vector<float>& w, int cout, int cin, int ntc, int cs_pad,
+                            std::vector<float>& blob, size_t off) {
+  const int ks_n = cs_pad / 16;
+  _Float16* dst = reinterpret_cast<_Float16*>(blob.data() + off);
+  bool ok = true;
+  for (int nt = 0; nt < cout / ntc; ++nt)
+    for (int ks = 0; ks < ks_n; ++ks)
+      for (int part = 0; part < 2; ++part)
+        for (int hh = 0; hh < 2; ++hh)
+          for (int col = 0; col < ntc; ++col)
+            for (int j = 0; j < 8; ++j) {
+              const int co = nt * ntc + col, ci = ks * 16 + hh * 8 + j;
+              const float v = ci < cin ? w[(size_t)co * cin + ci] : 0.f;
+              const _Float16 hi = (_Float16)v;
+              _Float16 o;
+              if (part == 0) {
+                const float sc = (float)hi * 2048.0f;
+                if (!(std::fabs(sc) <= 65504.0f)) ok = false;
+                o = (_Float16)sc;
+              } else {
+                o = (_Float16)((v - (float)hi) * 2048.0f);
+              }
+              dst[(((((size_t)nt * ks_n + ks) * 2 + part) * 2 + hh) * ntc + col) * 8 + j] = o;
+            }
+  return ok;
+}
+
 // K chunks of a conv on the split kernel: 16-channel 3x3 chunks + kSkipChunk-channel 1x1 skip chunks; a
 // plain 1x1 conv (attention qkv / proj_out) runs as skip chunks only
 static int x3_nchunks(const ConvW& cw) {
@@ -463,6 +503,17 @@ int Model::finalize() {
     } else if (c.taps == 1 && c.bn == 64 && c.cin_pad % kSkipChunk == 0 && !c.has_skip) {
       c.x3s_off = reserve((size_t)c.cout_pad * c.cin_pad);  // a 1x1 conv runs as 1x1 chunks only
     }
+    c.x3w_off = 0;
+    if (c.x3_off && c.taps == 9 && c.cout % 128 == 0 && c.cout == c.cout_pad)
+      c.x3w_off = reserve((size_t)c.cout_pad * c.cin_pad * c.taps);
+    c.sk_off = c.bmain_off = c.sbias_off = 0;
+    c.sk_ntc = 0;
+    if (c.has_skip && c.x3_off && c.cout == c.cout_pad) c.sk_ntc = skip_x3_ntc(c.cs_pad, c.cout);
+    if (c.sk_ntc) {
+      c.sk_off = reserve((size_t)c.cout * c.cs_pad);
+      c.bmain_off = reserve(c.cout_pad);
+      c.sbias_off = reserve(c.cout_pad);
+    }
   };
   auto plan_gn = [&](GNW& g) {
     g.g_off = reserve(g.C);
@@ -503,6 +554,8 @@ int Model::finalize() {
     pack_conv(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob, c.w_off);
     c.x3_ok = c.x3_off && pack_conv_x3(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob,
                                        c.x3_off);
+    if (c.x3_ok && c.x3w_off)  // (same weights and range check as the BN = 64 packing)
+      (void)pack_conv_x3(host_[c.wname], c.cout, c.cin, c.taps, 128, c.cin_pad, c.cout_pad, blob, c.x3w_off);
     if (c.taps == 1 && c.x3s_off)
       c.x3_ok = pack_skip_x3(host_[c.wname], c.cout, c.cin, c.bn, c.cin_pad, c.cout_pad, blob, c.x3s_off);
     if (c.x3_ok && c.has_skip)
@@ -514,6 +567,15 @@ int Model::finalize() {
       const auto& sb = host_[c.sbname];
       // bias of h (conv) and of skip_connection(x) are both added once per output element
       for (int i = 0; i < c.cout; ++i) blob[c.b_off + i] = b[i] + sb[i];
+    }
+    c.sk_ok = false;
+    if (c.sk_ntc) {
+      c.sk_ok = c.x3_ok && pack_skip1x1_x3(host_[c.swname], c.cout, c.cs, c.sk_ntc, c.cs_pad, blob, c.sk_off);
+      const auto& sb = host_[c.sbname];
+      for (int i = 0; i < c.cout; ++i) {
+        blob[c.bmain_off + i] = b[i];
+        blob[c.sbias_off + i] = sb[i];
+      }
     }
   };
   auto fill_gn = [&](GNW& g) {
@@ -554,6 +616,15 @@ int Model::finalize() {
     fill_conv(r.conv1);
     fill_gn(r.gn2);
     fill_conv(r.conv2);
+    r.conv2_res = r.conv2;
+    if (r.conv2.sk_ok) {  // the same conv without its 1x1 segment, own bias only
+      ConvW& c = r.conv2_res;
+      c.has_skip = false;
+      c.cs = c.cs_pad = 0;
+      c.ws_off = c.x3s_off = 0;
+      c.b_off = c.bmain_off;
+      c.sk_ok = false;
+    }
   }
   for (auto& a : attn_) {
     fill_gn(a.gn);
@@ -648,6 +719,7 @@ size_t Model::plan_workspace(int B, WsLayout& w, std::vector<std::pair<size_t, s
       const int H = r.xf == XF_UP ? 2 * L.res_in : (r.xf == XF_DOWN ? L.res_in / 2 : L.res_in);
       consider(r.conv1, H);
       consider(r.conv2, H);
+      if (r.conv2.sk_ok) consider(r.conv2_res, H);  // (the separate-skip plan's conv2)
     } else {
       consider(attn_[L.idx].qkv, L.res_in);
       consider(attn_[L.idx].proj, L.res_in);
@@ -832,9 +904,20 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   const bool x3_masked = x3_masked_for(p);
   const bool use_x3 = split_ && cw.x3_ok && !x3_masked && conv_x3_eligible(p, cw.taps, xf, cw.bn);
   IFD_REQUIRE(use_x3 || p.cin_pad == cw.cin_pad, "1x1-only operand rewrite without the split kernel");
+  bool use_x3w = false;
   if (use_x3) {
     p.wpack = wblob_ + cw.x3_off;
     if (cw.has_skip) p.wskip = wblob_ + cw.x3s_off;
+    // the wide-unit kernel for the large layers with 128-multiple widths (conv_x3w.hip)
+    if (cw.x3w_off && !cw.has_skip && opt_x3w_ > 0 && H >= opt_x3w_ && !(x3_off & 64)) {
+      ConvParams q = p;
+      conv_x3w_geometry(q, H, H, N);
+      q.wpack = wblob_ + cw.x3w_off;
+      if (conv_x3w_eligible(q, cw.taps, xf)) {
+        p = q;
+        use_x3w = true;
+      }
+    }
   } else if (x3_geo) {  // not split-eligible after all: the fp32 kernels' own geometry
     conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8);
   }
@@ -851,7 +934,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     auto it = stat_area_.find(out);
     if (it != stat_area_.end()) {
       p.gstat = it->second;
-      p.gstat_E = p.tiles_x * p.tiles_y * (use_stream ? 4 : 1);
+      p.gstat_E = p.tiles_x * p.tiles_y * (use_stream && !use_x3w ? 4 : 1);
     }
   }
 #if IFD_TRACE
@@ -887,8 +970,10 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                    (cw.has_skip ? pix * cw.cs : 0) + (res ? pix * cw.cout : 0));
     if (prof_layers_)
       snprintf(nm, sizeof(nm), "%s<%d,%d,%d,%d> r%d %d+%d->%d skip%d",
-               use_x3 ? "conv_x3" : (use_head ? "conv_head" : (use_stream ? "conv_stream" : "conv_kernel")), p.bm,
+               use_x3w ? "conv_x3w" : use_x3 ? "conv_x3" : (use_head ? "conv_head" : (use_stream ? "conv_stream" : "conv_kernel")), p.bm,
                cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
+    else if (use_x3w)
+      snprintf(nm, sizeof(nm), "conv_x3w_kernel<%d,%d>", xf, p.x3_nprod);
     else if (use_x3)
       snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d,%d>", xf, cw.has_skip ? "true" : "false", p.TW, p.x3_nprod);
     else if (use_head_x3)
@@ -906,13 +991,14 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   hipEvent_t e0;
   prof_begin(s, &e0, nm);
   if (use_head) p.ksplit = 1;
-  int e = use_x3       ? launch_conv_x3(p, xf, s)
+  int e = use_x3w      ? launch_conv_x3w(p, xf, s)
+          : use_x3     ? launch_conv_x3(p, xf, s)
           : use_head_x3 ? launch_conv_head_x3(p, wblob_ + cw.head_x3_off, s)
           : use_head   ? launch_conv_head(p, wblob_ + cw.head_off, s)
           : use_stream ? launch_conv_stream(p, xf, stream_mode, s)
                        : launch_conv(p, cw.taps, xf, cw.bn, s);
   if (p.gstat)
-    stat_[out] = StatRec{p.gstat, p.gstat_E, 4.0f * (use_stream ? 64 : p.bm), cw.cout};
+    stat_[out] = StatRec{p.gstat, p.gstat_E, 4.0f * (use_x3w ? p.bm : use_stream ? 64 : p.bm), cw.cout};
   else
     stat_.erase(out);
 #if IFD_TRACE
@@ -1010,6 +1096,42 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
   e = run_gn(t1, r.cout, nullptr, 0, N, H * H, r.gn2, ws_ + ly_.o_E_, emb_total_, r.emb_off, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, H * H, r.cout));
   IFD_REQUIRE(e == 0, "gn launch");
+  // split modes: skip_connection(x) as its own launch into `out`, then conv2 adds it as its residual
+  // in place (each output element's residual is read by the thread that writes it)
+  const bool split_mode = prec_ == IFD_PREC_3XF16 || prec_ == IFD_PREC_F16;
+  if (split_mode && r.conv2.sk_ok && r.xf == XF_NONE && opt_skip_sep_ > 0 && H >= opt_skip_sep_ &&
+      !(opt_x3_off_ & 4)) {
+    Skip1x1Params q;
+    q.s0 = in0; q.sc0 = c0; q.s1 = in1; q.sc1 = in1 ? c1 : 0;
+    q.npix = N * H * H;
+    q.cout = r.cout;
+    q.wpack = wblob_ + r.conv2.sk_off;
+    q.bias = wblob_ + r.conv2.sbias_off;
+    q.out = out;
+    q.guard = guard_;
+    q.ntc = r.conv2.sk_ntc;
+    q.nprod = prec_ == IFD_PREC_F16 ? 1 : 3;
+    if (skip_x3_eligible(q)) {
+      char nm[96] = "";
+      const double pix = (double)N * H * H;
+      if (prof_on_) {
+        if (prof_layers_)
+          snprintf(nm, sizeof(nm), "skip_x3 r%d %d+%d->%d", H, c0, q.sc1, r.cout);
+        else
+          snprintf(nm, sizeof(nm), "skip_x3_kernel<%d,%d>", q.ntc, q.nprod);
+      }
+      hipEvent_t e0;
+      prof_begin(s, &e0, nm);
+      const int e2 = launch_skip_x3(q, s);
+      if (prof_on_ && e0) prof_end(s, e0, nm, 2.0 * pix * r.cout * (c0 + q.sc1), 4.0 * pix * (c0 + q.sc1 + r.cout));
+      if (e2) {
+        set_error(std::string("skip launch failed: ") + hipGetErrorString((hipError_t)e2));
+        return 1;
+      }
+      return run_conv(r.conv2_res, t1, r.cout, nullptr, 0, N, H, H, XF_NONE, ACT_AFFINE_SILU, A, Bc, nullptr, 0,
+                      nullptr, 0, out, XF_NONE, H, out, EPI_NHWC, s);
+    }
+  }
   const float* res = r.conv2.has_skip ? nullptr : in0;
   return run_conv(r.conv2, t1, r.cout, nullptr, 0, N, H, H, XF_NONE, ACT_AFFINE_SILU, A, Bc, in0, c0, in1, c1, res,
                   r.xf, Hin, out, EPI_NHWC, s);

@@ -43,6 +43,10 @@ TRAIN_EXPORTS = {
                                    vp, vp, vp]),
     "ifd_tr_gn_fwd_gstat": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, i32, vp, i32, f32, vp, vp, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
+    "ifd_tr_x3w_pack_bytes": (i64, [i32, i32]),
+    "ifd_tr_pack_conv_x3w": (i32, [vp, i32, i32, i32, vp, vp, vp]),
+    "ifd_tr_conv_x3w": (i32, [vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, i64,
+                              vp, vp, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
     "ifd_tr_conv_wgrad": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp]),

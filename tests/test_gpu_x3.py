@@ -71,6 +71,54 @@ def test_x3_unet_full(evals, x3_model, record):
     assert err <= 1e-5
 
 
+@pytest.mark.parametrize("skip_sep", [8, 0])
+def test_x3_skip_launch(evals, x3_model, record, skip_sep):
+    """ResBlock skip_connection (code/nn.py:184, added at :212) as its own split-MFMA launch
+    (skip_x3_kernel; the default plan runs it at >= 64^2) against the reference output, and against
+    the other plans of the same weights: skip_sep=8 runs every skip layer through it (all three
+    output-channel tile widths), skip_sep=0 keeps the 1x1 segment fused into conv2's launch."""
+    from ifd.model import DiffusionInpaintingModel
+    x, gt, mask = (_t(evals[f"full/{k}"]).to(DEV) for k in ("x", "gt", "mask"))
+    t = torch.tensor([999], device=DEV)
+    m = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16", options={"skip_sep": skip_sep})
+    m.load_state_dict(make_state_dict(FULL, seed=1))
+    with torch.no_grad():
+        y_def, ks = _kernels_run(x3_model, lambda: x3_model(x, t, masked_image=gt * (1 - mask), mask=mask))
+        y, ks2 = _kernels_run(m, lambda: m(x, t, masked_image=gt * (1 - mask), mask=mask))
+    assert any(k.startswith("skip_x3_kernel<128,3>") for k in ks), sorted(ks)
+    if skip_sep == 8:
+        assert {"skip_x3_kernel<128,3>", "skip_x3_kernel<64,3>", "skip_x3_kernel<32,3>"} <= set(ks2), sorted(ks2)
+    else:
+        assert not any(k.startswith("skip_x3") for k in ks2), sorted(ks2)
+    ref = _t(evals["full_t999/y"])
+    e_def, e = maxabs(y_def, ref), maxabs(y, ref)
+    record(f"unet_full_t999/3xf16/skip_sep{skip_sep}", maxabs=e, maxabs_default_plan=e_def)
+    assert e_def <= 1e-5 and e <= 1e-5
+    assert maxabs(y, y_def) <= 2e-5
+
+
+@pytest.mark.parametrize("x3w", [16, 0])
+def test_x3_wide_units(evals, x3_model, record, x3w):
+    """The wide-unit 3x3 kernel (conv_x3w_kernel: 8x16 pixels x 128 output channels per unit, the
+    default plan's kernel for the 128-multiple-width layers at >= 64^2) against the reference output;
+    x3w=16 also runs it on the 32^2 and 16^2 layers, x3w=0 keeps every layer on conv_x3_kernel."""
+    from ifd.model import DiffusionInpaintingModel
+    x, gt, mask = (_t(evals[f"full/{k}"]).to(DEV) for k in ("x", "gt", "mask"))
+    t = torch.tensor([999], device=DEV)
+    m = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16", options={"x3w": x3w})
+    m.load_state_dict(make_state_dict(FULL, seed=1))
+    with torch.no_grad():
+        y_def, ks = _kernels_run(x3_model, lambda: x3_model(x, t, masked_image=gt * (1 - mask), mask=mask))
+        y, ks2 = _kernels_run(m, lambda: m(x, t, masked_image=gt * (1 - mask), mask=mask))
+    assert {"conv_x3w_kernel<0,3>", "conv_x3w_kernel<1,3>"} <= set(ks), sorted(ks)
+    assert any(k.startswith("conv_x3w") for k in ks2) == (x3w > 0), sorted(ks2)
+    ref = _t(evals["full_t999/y"])
+    e_def, e = maxabs(y_def, ref), maxabs(y, ref)
+    record(f"unet_full_t999/3xf16/x3w{x3w}", maxabs=e, maxabs_default_plan=e_def)
+    assert e_def <= 1e-5 and e <= 1e-5
+    assert maxabs(y, y_def) <= 2e-5
+
+
 def test_x3_matches_fp32_batch(x3_model):
     """B=3 random inputs (tile counts not a multiple of the grid) at three timesteps: the split
     mode against the fp32 mode of the same weights."""
