@@ -17,15 +17,19 @@
 // 32 w .. 32 w + 31 of the unit, and its B fragments are private to it. Each consumer loads them
 // from L2 straight into registers (two 1-KiB wave loads per tap, 18 per chunk, 72 VGPRs), one chunk
 // ahead: right after a tap's last MFMA group has issued, the same registers are reloaded with the
-// next chunk's fragments of that tap. LDS holds only the two halo stages (22.5 KiB); one barrier per
+// next chunk's fragments of that tap. LDS holds the halo stages and the residual; one barrier per
 // chunk hands a stage from the producers to the consumers.
 //   * waves 0-3 consumers: wave w = 128 pixels (4 blocks of 32, rows 2 mr, 2 mr + 1 of the tile) x
-//     32 channels; per tap 8 A-fragment ds_read_b128 (hi / lo x 4 pixel blocks) and 12
-//     v_mfma_f32_32x32x16_f16 in three groups of four independent accumulators.
+//     32 channels; per tap 8 A-fragment ds_read_b128 (hi / lo x 4 pixel blocks, double-buffered by
+//     tap parity) and 12 v_mfma_f32_32x32x16_f16 in three groups of four independent accumulators.
+//     The stages are written two chunks ahead, so a chunk's tap-0 fragments are read during the
+//     previous chunk's last tap instead of after the barrier. The residual arrives by LDS-DMA during
+//     the unit's last chunks (no registers held for it).
 //   * waves 4-7 producers: thread t stages channel quarter t & 3 of halo pixels t / 4 + 64 k
 //     (k < 3): one 16-B load per item, the GroupNorm coefficients of its quarter (two 16-B loads),
-//     registers two chunks ahead, the prologue + split one chunk ahead, 8-B LDS writes.
-// LDS: A = [part hi / lo][channel half h][180 halo px][8 f16] (11.25 KiB) x 2 stages.
+//     registers two intervals ahead, the prologue + split two chunks ahead, 8-B LDS writes.
+// LDS: A = [part hi / lo][channel half h][180 halo px][8 f16] (11.25 KiB) x 3 stages + 4 x 16 KiB of
+// residual.
 #include "conv.h"
 #include "conv_dev.h"
 
@@ -44,7 +48,9 @@ constexpr int WHW = WTW + 2;              // halo row width
 constexpr int WNP = WHW * (WTH + 2);      // 180 halo pixels
 constexpr int WBN = 128;                  // output channels per unit
 constexpr int WA = 4 * WNP * 4;           // floats per A stage (4 planes x 180 px x 16 B)
-constexpr int W_LDS_FLOATS = 2 * WA;      // 23,040 B
+constexpr int WST = 3;                    // A stages (the consumers read a chunk's tap 0 an interval early)
+constexpr int WRES = 64 * 64;             // residual floats per consumer wave (64 registers x 64 lanes)
+constexpr int W_LDS_FLOATS = WST * WA + 4 * WRES;  // 34,560 + 65,536 B
 constexpr int WIT = 3;                    // quarter-pixel items per producer thread (4 x 180 = 720 <= 3 x 256)
 constexpr float kLo = 2048.0f;            // 2^11
 constexpr int WPF = 2;                    // residual / bias prefetch: chunks before the unit's end
@@ -55,7 +61,14 @@ static_assert(4 * WNP <= WIT * NP_T, "producer items");
 // Timing-only ablation builds (never shipped; outputs are garbage): X3W_ABLATE=
 //   1 producers write the raw bits (no prologue / split VALU)   2 consumers skip the B reloads
 //   3 consumers skip the A reads after a chunk's tap 0          4 producers idle (barriers only)
-//   5 consumers skip the MFMAs
+//   5 consumers skip the MFMAs   6 SiLU replaced by the affine value (no exp / rcp)
+//   7 lo part not computed (zero) and no range guard   8 no range guard
+//   9 exp and rcp replaced by 8-FMA chains each (same dependency depth class, no transcendental)
+// IFD_TRACE=1 builds: consumer wave 0 of each block stamps (s_memtime, s_memrealtime) at its start and
+// end into ConvParams::trace[64 b + 0..3] (the shader clock over the launch = d memtime / d realtime x 100 MHz)
+#ifndef IFD_TRACE
+#define IFD_TRACE 0
+#endif
 #ifndef X3W_ABLATE
 #define X3W_ABLATE 0
 #endif
@@ -70,6 +83,47 @@ __device__ __forceinline__ void split2w(float v0, float v1, unsigned& h, unsigne
       "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
       : "=&v"(l)
       : "v"(v0), "v"(v1), "v"(h));
+}
+
+// SiLU of the GroupNorm-applied value t: t * rcp(1 + 2^(-t log2 e)), padding (pinf = +inf) -> 0.
+// X3W_SILU selects how the two reciprocal / exponential steps are computed:
+//   0 v_exp_f32 + v_rcp_f32 (two transcendentals)
+//   1 polynomial 2^x + v_rcp_f32     2 v_exp_f32 + Newton reciprocal     3 neither (full-rate VALU only)
+// The polynomial: x clamped to [-126, 126] (a padding value, x = +inf, then gives t * 2^-126, which the
+// f16 split rounds to exactly 0, as it does every |v| < 2^-25), n = rint(x) by the 1.5 * 2^23 shifter,
+// 2^(x - n) by a degree-6 fit on [-1/2, 1/2] (max rel. error 1.0e-7), 2^n built in the exponent field.
+// The Newton reciprocal: seed 0x7EF311C3 - bits(d) (rel. error <= 12 %), three steps r += r (1 - d r)
+// (<= 4e-8).
+#ifndef X3W_SILU
+#define X3W_SILU 0
+#endif
+__device__ __forceinline__ float exp2_poly(float x) {
+  x = __builtin_amdgcn_fmed3f(x, -126.0f, 126.0f);
+  const float sh = 12582912.0f;  // 1.5 * 2^23
+  const float y = x + sh;
+  const float f = x - (y - sh);
+  float p = 1.5337577497120947e-04f;
+  p = fmaf(p, f, 1.3399859890341759e-03f);
+  p = fmaf(p, f, 9.618519805371761e-03f);
+  p = fmaf(p, f, 5.550329014658928e-02f);
+  p = fmaf(p, f, 2.4022646248340607e-01f);
+  p = fmaf(p, f, 6.931471824645996e-01f);
+  p = fmaf(p, f, 1.0f);
+  // bits(y) = 0x4B400000 + n  ->  bits(2^n) = (n + 127) << 23
+  const unsigned sc = (__builtin_bit_cast(unsigned, y) << 23) + ((127u - 0x4B400000u) << 23);
+  return p * __builtin_bit_cast(float, sc);
+}
+__device__ __forceinline__ float rcp_newton(float d) {
+  float r = __builtin_bit_cast(float, 0x7EF311C3u - __builtin_bit_cast(unsigned, d));
+#pragma unroll
+  for (int i = 0; i < 3; ++i) r = fmaf(r, fmaf(-d, r, 1.0f), r);
+  return r;
+}
+__device__ __forceinline__ float silu_w(float t, float pinf) {
+  const float x = fmaf(t, -1.4426950408889634f, pinf);
+  const float e = (X3W_SILU & 1) ? exp2_poly(x) : __builtin_amdgcn_exp2f(x);
+  const float d = 1.0f + e;
+  return t * ((X3W_SILU & 2) ? rcp_newton(d) : __builtin_amdgcn_rcpf(d));
 }
 
 __device__ __forceinline__ f32x16 wmfma(f16x8 a, f16x8 b, f32x16 c) {
@@ -188,7 +242,20 @@ struct WProducer {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const float t = fmaf(s.ca[c], s.raw[k][c], s.cb[c]);
-          v[c] = t * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(fmaf(t, -1.4426950408889634f, pinf)));
+          if (X3W_ABLATE == 6)
+            v[c] = fmaf(t, 0.5f, pinf);
+          else if (X3W_ABLATE == 9) {
+            float e = fmaf(t, -1.4426950408889634f, pinf);
+            float a = e;
+#pragma unroll
+            for (int z = 0; z < 8; ++z) a = fmaf(a, e, 0.3f);
+            float d = 1.0f + a, r = d;
+#pragma unroll
+            for (int z = 0; z < 8; ++z) r = fmaf(r, d, -0.7f);
+            v[c] = t * r;
+          }
+          else
+            v[c] = silu_w(t, pinf);
         }
       } else if (ACT == ACT_AFFINE) {
 #pragma unroll
@@ -198,7 +265,8 @@ struct WProducer {
         for (int c = 0; c < 4; ++c) v[c] = s.raw[k][c] * s.vld[k];
       }
       // range guard: |v| >= 65504 would split into an f16 inf
-      gmax = fmaxf(gmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+      if (X3W_ABLATE != 7 && X3W_ABLATE != 8)
+        gmax = fmaxf(gmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
       unsigned h0, h1, l0, l1;
       lds_f* dst = As + 4 * (hh * WNP + px[k]) + 2 * sub;
       if (NPROD == 1) {
@@ -209,8 +277,14 @@ struct WProducer {
         *(lds_u2*)dst = u32x2{h0, h1};
         continue;
       }
-      split2w(v[0], v[1], h0, l0);
-      split2w(v[2], v[3], h1, l1);
+      if (X3W_ABLATE == 7) {
+        h0 = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{v[0], v[1]}, f16x2));
+        h1 = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{v[2], v[3]}, f16x2));
+        l0 = l1 = 0;
+      } else {
+        split2w(v[0], v[1], h0, l0);
+        split2w(v[2], v[3], h1, l1);
+      }
       *(lds_u2*)dst = u32x2{h0, h1};
       *(lds_u2*)(dst + 4 * 2 * WNP) = u32x2{l0, l1};
     }
@@ -245,9 +319,13 @@ __global__ __launch_bounds__(NT, 2) void conv_x3w_kernel(ConvParams p) {
   const int lnct = __builtin_ctz(nct), ltx = __builtin_ctz(p.tiles_x), lty = __builtin_ctz(p.tiles_y);
   const int G = gridDim.x, b = blockIdx.x;
   const int nu = ((p.npix_tiles - b + G - 1) / G) << lnct;  // host: grid <= npix_tiles
-  const int nch = p.cin_pad / 16;
+  const int nch = p.cin_pad / 16;                            // host: even
   const int J = nu * nch;
 
+  if (IFD_TRACE && p.trace && tid == 0) {
+    p.trace[64 * b + 0] = __builtin_amdgcn_s_memtime();
+    p.trace[64 * b + 1] = __builtin_amdgcn_s_memrealtime();
+  }
   if (wave < 4) {
     // ---------------- consumers ----------------
     const int h = lane >> 5, l32 = lane & 31;
@@ -280,63 +358,55 @@ __global__ __launch_bounds__(NT, 2) void conv_x3w_kernel(ConvParams p) {
     auto roff = [&](int r) { return (((r >> 3) * p.W) + 8 * ((r >> 2) & 1) + (r & 3)) * p.cout * 4; };
     const int mstep = 2 * p.W * p.cout * 4;
     auto vbase = [&](const WUnit& t) { return (((t.y0 * p.W) + t.x0 + 4 * h) * p.cout + t.ct * WBN + 32 * wave + l32) * 4; };
-    // residual of pixel blocks mr0, mr0 + 1 into rv (32 registers: the blocks 0-1 are prefetched
-    // during the unit's last chunks, the blocks 2-3 load while 0-1 are stored)
-    float rv[2][16];
+    // The residual goes HBM -> LDS by DMA (buffer_load ... lds) during the unit's last chunks: register
+    // (mr, r) of every lane lands at Rw[(16 mr + r) * 64 + lane] (64 dword DMAs of 256 B), read back in
+    // the epilogue; no registers are held for it across the chunks.
+    lds_f* const Rw = A0 + WST * WA + wave * WRES;
     float bias = 0.f;
-    auto res_load = [&](const WUnit& t, int mr0) __attribute__((always_inline)) {
-      const rsrc_t rr = mkrsrc(p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout);
-      if (p.res_xform == XF_NONE) {
-        const int vb = vbase(t);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            rv[i][r] =
-                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb + (mr0 + i) * mstep, roff(r), 0));
-      } else {  // XF_UP: nearest-upsampled residual
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int mr = mr0 + i;
-            const int y = (t.y0 + 2 * mr + (r >> 3)) >> 1, x = (t.x0 + 8 * ((r >> 2) & 1) + 4 * h + (r & 3)) >> 1;
-            const int o = ((y * p.res_W + x) * p.cout + t.ct * WBN + 32 * wave + l32) * 4;
-            rv[i][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, o, 0, 0));
-          }
-      }
-    };
     auto prefetch = [&](const WUnit& t) {
       bias = gld1(p.bias + t.ct * WBN + 32 * wave + l32);
-      if (p.res) res_load(t, 0);
+      if (!p.res) return;
+      const rsrc_t rr = mkrsrc(p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout);
+      const int vb = vbase(t);
+#pragma unroll
+      for (int mr = 0; mr < 4; ++mr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          auto* dst = (__attribute__((address_space(3))) void*)(Rw + (16 * mr + r) * 64);
+          if (p.res_xform == XF_NONE) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, dst, 4, vb + mr * mstep, roff(r), 0, 0);
+          } else {  // XF_UP: nearest-upsampled residual
+            const int y = (t.y0 + 2 * mr + (r >> 3)) >> 1, x = (t.x0 + 8 * ((r >> 2) & 1) + 4 * h + (r & 3)) >> 1;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, dst, 4, ((y * p.res_W + x) * p.cout + t.ct * WBN + 32 * wave + l32) * 4,
+                                                     0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);  // one address at a time (64 hoisted ones would spill)
+          }
+        }
     };
     auto epilogue = [&](const WUnit& t) {
       const size_t img = (size_t)p.H * p.W * p.cout;
       const rsrc_t ro = mkrsrc(p.out + (size_t)t.n0 * img);
       const int vb = vbase(t);
+      // the residual DMA (not in hipcc's vmcnt model) was issued before the B loads of the unit's last
+      // WPF chunks (18 per chunk, 9 in the f16 mode): wait until only those are outstanding
+      static_assert(WPF == 2, "vmcnt literal");
+      if (p.res) {
+        if (NPROD == 3)
+          asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+      }
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
+      for (int mr = 0; mr < 4; ++mr) {  // one pixel block at a time (bounds the residual values in flight)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int mr = 2 * half + i;
-            float x = acc[mr][r] * (1.0f / kLo);  // exact rescale
-            x = x + bias;
-            if (p.res) x = rv[i][r] + x;  // torch order: x_res + (conv + bias)
-            acc[mr][r] = x;
-          }
-        if (half == 0 && p.res) res_load(t, 2);  // blocks 2-3 (the values above hold blocks 0-1)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-          {
-            // (a named float: __builtin_bit_cast of a vector-element lvalue reads element 0)
-            const float v = acc[2 * half + i][r];
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ro, vb + (2 * half + i) * mstep,
-                                                  roff(r), 0);
-          }
+        for (int r = 0; r < 16; ++r) {
+          float x = acc[mr][r] * (1.0f / kLo);  // exact rescale
+          x = x + bias;
+          if (p.res) x = Rw[(16 * mr + r) * 64 + lane] + x;  // torch order: x_res + (conv + bias)
+          acc[mr][r] = x;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep, roff(r), 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
       if (p.gstat) {
         // granule statistics of 4 channels x the tile's 128 pixels: this lane's 64 (two-pass), the
@@ -378,45 +448,46 @@ __global__ __launch_bounds__(NT, 2) void conv_x3w_kernel(ConvParams p) {
         }
       }
     };
-    // one chunk's MFMAs; the B registers of tap t are reloaded with (nct_, nch_)'s tap t after use
-    // one chunk's MFMAs; the B registers of tap t are reloaded with (nxt_ct, nxt_ch)'s tap t after use.
-    // A fragments single-buffered: a tap's hi fragments are re-read for the next tap once its last hi
-    // MFMA group has issued (MFMAs read SrcA / SrcB at issue; only SrcC has a WAR window)
-    auto chunk = [&](const lds_f* As, int nxt_ct, int nxt_ch) __attribute__((always_inline)) {
+    // A fragments: the hi parts double-buffered by tap parity (the slot sequence runs on across chunks:
+    // 9 taps, chunk parity sb = slot of its tap 0), the lo parts single: the next tap's hi reads go out
+    // right after the current tap's hi x hi group and its lo reads after the lo x hi group, each 8
+    // MFMAs ahead of use. The last tap reads the next chunk's tap 0 from its stage, which the producers
+    // completed an interval earlier (three stages).
+    f16x8 ah[2][4], al[4];
+    auto afetch_hi = [&](const lds_f* As, int tap, int slot) __attribute__((always_inline)) {
+      if (X3W_ABLATE == 3 && tap > 0) return;
       const lds_f* Ah = As + 4 * (h * WNP);
-      const lds_f* Al = As + 4 * ((2 + h) * WNP);
-      f16x8 ah[4], al[4];
+      const int toff = tap / 3 * WHW + tap % 3;
 #pragma unroll
-      for (int mr = 0; mr < 4; ++mr) {
-        ah[mr] = *(const lds_h8*)(Ah + 4 * pb[mr]);
-        if (NPROD == 3) al[mr] = *(const lds_h8*)(Al + 4 * pb[mr]);
-      }
+      for (int mr = 0; mr < 4; ++mr) ah[slot][mr] = *(const lds_h8*)(Ah + 4 * (pb[mr] + toff));
+    };
+    auto afetch_lo = [&](const lds_f* As, int tap) __attribute__((always_inline)) {
+      if (NPROD == 1 || (X3W_ABLATE == 3 && tap > 0)) return;
+      const lds_f* Al = As + 4 * ((2 + h) * WNP);
+      const int toff = tap / 3 * WHW + tap % 3;
+#pragma unroll
+      for (int mr = 0; mr < 4; ++mr) al[mr] = *(const lds_h8*)(Al + 4 * (pb[mr] + toff));
+    };
+    auto chunk = [&](const lds_f* As, const lds_f* An, int sb, int nxt_ct, int nxt_ch) __attribute__((always_inline)) {
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const int tn = (tap + 1) / 3 * WHW + (tap + 1) % 3;  // next tap's halo offset
+        const int cur = (sb + tap) & 1;
+        const lds_f* Sn = tap + 1 < 9 ? As : An;
+        const int tn = tap + 1 < 9 ? tap + 1 : 0;
 #pragma unroll
-        for (int mr = 0; mr < 4; ++mr) acc[mr] = wmfma(ah[mr], bh[tap], acc[mr]);
+        for (int mr = 0; mr < 4; ++mr) acc[mr] = wmfma(ah[cur][mr], bh[tap], acc[mr]);
+        __builtin_amdgcn_sched_barrier(0);
+        afetch_hi(Sn, tn, cur ^ 1);
         __builtin_amdgcn_sched_barrier(0);
         if (NPROD == 3) {
 #pragma unroll
-          for (int mr = 0; mr < 4; ++mr) acc[mr] = wmfma(ah[mr], bl[tap], acc[mr]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (tap + 1 < 9 && X3W_ABLATE != 3) {
-#pragma unroll
-          for (int mr = 0; mr < 4; ++mr) ah[mr] = *(const lds_h8*)(Ah + 4 * (pb[mr] + tn));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (NPROD == 3) {
+          for (int mr = 0; mr < 4; ++mr) acc[mr] = wmfma(ah[cur][mr], bl[tap], acc[mr]);
 #pragma unroll
           for (int mr = 0; mr < 4; ++mr) acc[mr] = wmfma(al[mr], bh[tap], acc[mr]);
-          __builtin_amdgcn_sched_barrier(0);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        afetch_lo(Sn, tn);
         bload(nxt_ct, nxt_ch, tap);
-        if (NPROD == 3 && tap + 1 < 9 && X3W_ABLATE != 3) {
-#pragma unroll
-          for (int mr = 0; mr < 4; ++mr) al[mr] = *(const lds_h8*)(Al + 4 * (pb[mr] + tn));
-        }
         __builtin_amdgcn_sched_barrier(0);
       }
     };
@@ -424,25 +495,38 @@ __global__ __launch_bounds__(NT, 2) void conv_x3w_kernel(ConvParams p) {
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) bload(t.ct, 0, tap);
     zero();
-    WBARRIER();  // chunk 0 staged
-    int j = 0;
+    WBARRIER();  // chunks 0 and 1 staged
+    afetch_hi(A0, 0, 0);
+    afetch_lo(A0, 0);
+    int sc = 0, sn = 1;  // stages of the current / next chunk
     for (int u = 0; u < nu; ++u) {
       const WUnit tn = u + 1 < nu ? w_unit(p, lnct, ltx, lty, b, u + 1) : t;
-      for (int c = 0; c < nch; ++c) {
-        if (c == (nch > WPF ? nch - WPF : 0)) prefetch(t);
-        const bool last = c + 1 == nch;
-        chunk(A0 + (j & 1) * WA, last ? tn.ct : t.ct, last ? 0 : c + 1);
-        ++j;
-        WBARRIER();
+      for (int c = 0; c < nch; c += 2) {
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int cc = c + half;
+          if (cc == nch - WPF) prefetch(t);
+          const bool last = cc + 1 == nch;
+          chunk(A0 + sc * WA, A0 + sn * WA, half, last ? tn.ct : t.ct, last ? 0 : cc + 1);
+          sc = sn;
+          sn = sn == WST - 1 ? 0 : sn + 1;
+          WBARRIER();
+        }
       }
       epilogue(t);
       zero();
       t = tn;
     }
+    if (IFD_TRACE && p.trace && tid == 0) {
+      p.trace[64 * b + 2] = __builtin_amdgcn_s_memtime();
+      p.trace[64 * b + 3] = __builtin_amdgcn_s_memrealtime();
+    }
     return;
   }
 
   // ---------------- producers ----------------
+  // interval j: prologue + split of chunk j + 2 into stage (j + 2) % 3 (its loads issued two intervals
+  // earlier), then the loads of chunk j + 4
   const int pt = tid - NP_T;
   WProducer<XF> P;
   P.init(pt);
@@ -461,20 +545,26 @@ __global__ __launch_bounds__(NT, 2) void conv_x3w_kernel(ConvParams p) {
         tl = w_unit(p, lnct, ltx, lty, b, ++ul);
       }
     } else {
-      jl += 2;  // past the end: the last chunk re-issued (identical bytes), never stored
+      jl += 2;  // past the end: the last chunk re-issued (identical bytes), never read
     }
   };
   issue(s0);  // chunk 0
   issue(s1);  // chunk 1
   P.template store<NPROD>(s0, p.act, A0);
+  issue(s0);  // chunk 2
+  P.template store<NPROD>(s1, p.act, A0 + WA);
+  issue(s1);  // chunk 3
   WBARRIER();
+  int sw = 2;  // stage of chunk j + 2
   for (int j = 0; j < J; j += 2) {
-    if (j + 1 < J) P.template store<NPROD>(s1, p.act, A0 + WA);  // chunk j+1
-    issue(s0);                                                    // chunk j+2
+    P.template store<NPROD>(s0, p.act, A0 + sw * WA);  // chunk j + 2 (past the end: an unread stage)
+    sw = sw == WST - 1 ? 0 : sw + 1;
+    issue(s0);  // chunk j + 4
     WBARRIER();
     if (j + 1 >= J) break;
-    if (j + 2 < J) P.template store<NPROD>(s0, p.act, A0);  // chunk j+2
-    issue(s1);                                              // chunk j+3
+    P.template store<NPROD>(s1, p.act, A0 + sw * WA);  // chunk j + 3
+    sw = sw == WST - 1 ? 0 : sw + 1;
+    issue(s1);  // chunk j + 5
     WBARRIER();
   }
   if (p.guard && P.gmax >= 65504.0f) atomicOr(p.guard, 1u);
@@ -510,6 +600,7 @@ void conv_x3w_geometry(ConvParams& p, int H, int W, int N) {
 
 bool conv_x3w_eligible(const ConvParams& p, int taps, int xform) {
   const int nct = p.cout / WBN;
+  if ((p.cin_pad / 16) % 2) return false;  // chunks run in pairs (A-fragment slot parity)
   return taps == 9 && (xform == XF_NONE || xform == XF_UP) && !p.wskip && p.epi == EPI_NHWC && p.ksplit == 1 &&
          p.TW == WTW && p.TH == WTH && p.IMGS == 1 && p.H % WTH == 0 && p.W % WTW == 0 &&
          (p.tiles_x & (p.tiles_x - 1)) == 0 && (p.tiles_y & (p.tiles_y - 1)) == 0 && p.cout % WBN == 0 &&

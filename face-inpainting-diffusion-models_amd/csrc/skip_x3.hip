@@ -35,7 +35,13 @@ constexpr int SK_NT = 512;  // threads per block (8 independent waves after the 
 #define SK_DEPTH 8
 #endif
 constexpr int SK_D = SK_DEPTH;  // k steps of operand in flight per wave
-constexpr int SK_LDS_MAX = 128 * 1024;
+#ifndef SK_LDS_KB
+#define SK_LDS_KB 128
+#endif
+#ifndef SK_WPE
+#define SK_WPE 2  // waves per SIMD the registers are budgeted for (blocks per CU = SK_WPE / 2)
+#endif
+constexpr int SK_LDS_MAX = SK_LDS_KB * 1024;
 constexpr float kScale = 2048.0f;  // 2^11
 
 // hi = f16(v) for the pair (one v_cvt_pk_f16_f32), lo = f16(v - hi) (v_fma_mix: v - hi exact in
@@ -55,7 +61,7 @@ __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
 }
 
 template <int NTC, int NPROD>
-__global__ __launch_bounds__(SK_NT, 2) void skip_x3_kernel(Skip1x1Params p) {
+__global__ __launch_bounds__(SK_NT, SK_WPE) void skip_x3_kernel(Skip1x1Params p) {
   constexpr int NR = NTC / 32;
   extern __shared__ __attribute__((aligned(16))) float smem_raw[];
   lds_u4* const W = (lds_u4*)smem_raw;  // [ks][part][h][NTC] x 16 B
@@ -192,7 +198,7 @@ int launch_inst(const Skip1x1Params& p, hipStream_t stream) {
   const int nnt = p.cout / NTC;
   const int ncu = device_cu_count();
   const int waves_needed = (p.npix / 32 + (SK_NT / 64) - 1) / (SK_NT / 64);  // blocks per channel tile
-  int per = ncu / nnt;
+  int per = ncu * (SK_WPE / 2) / nnt;
   if (per < 1) per = 1;
   if (per > waves_needed) per = waves_needed;
   hipLaunchKernelGGL((skip_x3_kernel<NTC, NPROD>), dim3(per * nnt), dim3(SK_NT), lds, stream, p);

@@ -177,7 +177,7 @@ class Model {
   int opt_lds_pad_ = 0;     // extra LDS bytes per fp32 conv block
   int opt_invariant_ = 0;   // batch-invariant geometry (results independent of the batch split)
   int opt_x3_order_ = 0;    // split kernel unit order (ConvParams::opt_x3_order)
-  int opt_x3w_ = 64;        // split modes: wide-unit 3x3 kernel at resolutions >= this (0 off)
+  int opt_x3w_ = 0;         // split modes: wide-unit 3x3 kernel at resolutions >= this (0 off)
   int opt_skip_sep_ = 64;   // split modes: ResBlock skip_connection as its own launch at resolutions >= this (0 off)
   void fill_opts(ConvParams& p) const {
     p.opt_x3_order = opt_x3_order_;

@@ -34,7 +34,7 @@ Model::Model(const ifd_config& cfg) : cfg_(cfg) {
   opt_invariant_ = env_int("IFD_BATCH_INVARIANT", 0) != 0;
   opt_x3_order_ = env_int("IFD_X3_ORDER", 0);
   opt_skip_sep_ = env_int("IFD_SKIP_SEP", 64);
-  opt_x3w_ = env_int("IFD_X3W", 64);
+  opt_x3w_ = env_int("IFD_X3W", 0);
 }
 
 int Model::set_option(const std::string& key, int v) {
