@@ -32,7 +32,7 @@ typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
 constexpr int SK_NT = 512;  // threads per block (8 independent waves after the weight load)
 #ifndef SK_DEPTH
-#define SK_DEPTH 8
+#define SK_DEPTH 4
 #endif
 constexpr int SK_D = SK_DEPTH;  // k steps of operand in flight per wave
 #ifndef SK_LDS_KB
