@@ -71,9 +71,22 @@ __global__ __launch_bounds__(SK_NT, SK_WPE) void skip_x3_kernel(Skip1x1Params p)
   const int bi = blockIdx.x / nnt, nb = gridDim.x / nnt;
   const int tid = threadIdx.x;
   {
-    const int n16 = KS * 4 * NTC;  // 16-B units of the tile's weights
+    // 16-B units of the tile's weights, eight loads in flight per thread
+    const int n16 = KS * 4 * NTC;
     const u32x4* src = (const u32x4*)p.wpack + (size_t)nt * n16;
-    for (int i = tid; i < n16; i += SK_NT) W[i] = *(__attribute__((address_space(1))) const u32x4*)(src + i);
+    for (int i0 = 0; i0 < n16; i0 += 8 * SK_NT) {
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + j * SK_NT + tid;
+        if (i < n16) v[j] = *(__attribute__((address_space(1))) const u32x4*)(src + i);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + j * SK_NT + tid;
+        if (i < n16) W[i] = v[j];
+      }
+    }
   }
   __syncthreads();  // the only barrier: the waves are independent from here on
 
