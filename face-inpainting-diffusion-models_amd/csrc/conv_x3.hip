@@ -468,6 +468,10 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   const int J = nu * nchu;
   const XDec dec = x3_dec(p, nct);
   auto unit_of = [&](int u, int& z) { return x3_unit<SKIP>(p, dec, (int)blockIdx.x, u, z); };
+  if (IFD_TRACE && p.trace && tid == 0) {  // block entry: real time (100 MHz) and shader cycles
+    p.trace[64 * blockIdx.x + 59] = __builtin_amdgcn_s_memrealtime();
+    p.trace[64 * blockIdx.x + 61] = __builtin_amdgcn_s_memtime();
+  }
 
   if (consumer) {
     const int h = lane >> 5, l32 = lane & 31;
@@ -739,6 +743,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
     };
     zero();
+    if (IFD_TRACE && p.trace && wave == 0 && lane == 0) p.trace[64 * blockIdx.x + 58] = __builtin_amdgcn_s_memtime();
     XBARRIER_CONSUMER();  // chunk 0 staged
     int j = 0;  // position in the block's chunk stream: ring slot j % 3, A stage j & 1
     for (int u = 0; u < nu; ++u) {
@@ -809,6 +814,10 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       zero();
     }
     if (SKIP && p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
+    if (IFD_TRACE && p.trace && wave == 0 && lane == 0) {  // consumer done (stores issued)
+      p.trace[64 * blockIdx.x + 60] = __builtin_amdgcn_s_memrealtime();
+      p.trace[64 * blockIdx.x + 62] = __builtin_amdgcn_s_memtime();
+    }
     return;
   }
 
@@ -872,18 +881,25 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         XBARRIER_PRODUCER(2);
     }
   };
+  auto fstamp = [&](int slot) {  // (trace builds: the pipeline fill)
+    if (IFD_TRACE && p.trace && ptid == 0) p.trace[64 * blockIdx.x + slot] = __builtin_amdgcn_s_memtime();
+  };
   issue(s0);  // chunk 0
+  fstamp(46);
   const int main0 = lastmain;
   issue(s1);  // chunk 1
+  fstamp(47);
   if (main0) P.store(s0, p.act, A0);  // (a split-K unit may start in the skip segment)
+  fstamp(56);
   barrier();
+  fstamp(57);
   // interval j: LDS writes of chunk j+1 (its loads were issued one interval ago), then the DMA and
   // halo loads of chunk j+2, then the barrier once chunk j+1's DMA (issued in interval j-1) has
   // landed. Writes BEFORE issue: hipcc's vmcnt model does not count LDS-DMA ops, so a wait for
   // chunk j+1's registers placed after chunk j+2's DMA would also wait for that DMA.
   auto stamp = [&](int slot, int j) {
-    // (slots of j >= 11 hold the consumer's first-epilogue stamps)
-    if (IFD_TRACE && p.trace && ptid == 0 && j < 11) p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
+    // (slots of j >= 8 hold the fill and the consumer's first-epilogue stamps)
+    if (IFD_TRACE && p.trace && ptid == 0 && j < 8) p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
   };
   for (int j = 0; j < J; j += 2) {
     if (j + 1 < J && lastmain) P.store(s1, p.act, A0 + XA);  // last issued = chunk j+1

@@ -319,6 +319,19 @@ __global__ __launch_bounds__(GN_NT) void gn_finalize2_kernel(GnFinalize2Params p
   const int C = p.s0.C + p.s1.C;
   const int Cg = C / GN_G;
   const int ng = Cg / 4;  // granules of the group
+  // the per-channel parameters are loaded before the reduction so their latency overlaps it
+  // (Cg <= GN_NT: one channel per thread)
+  const int cc = g * Cg + tid;
+  const bool has_c = tid < Cg;
+  float gam = 0.f, bet = 0.f, esc = 0.f, esh = 0.f;
+  if (has_c) {
+    gam = p.gamma[cc];
+    bet = p.beta[cc];
+    if (p.emb) {
+      esc = p.emb[(size_t)n * p.emb_stride + p.emb_off + cc];
+      esh = p.emb[(size_t)n * p.emb_stride + p.emb_off + C + cc];
+    }
+  }
   double sn = 0.0, sm = 0.0, sq = 0.0;
   for (int k = 0; k < ng; ++k) {
     const int c = g * Cg + 4 * k;
@@ -344,18 +357,17 @@ __global__ __launch_bounds__(GN_NT) void gn_finalize2_kernel(GnFinalize2Params p
   const double m2 = fmax(sq - ntot * mean * mean, 0.0);
   const float meanf = (float)mean;
   const float rstd = (float)(1.0 / sqrt(m2 / ntot + (double)p.eps));
-  for (int c = g * Cg + tid; c < (g + 1) * Cg; c += GN_NT) {
-    const float a = rstd * p.gamma[c];
-    const float b = p.beta[c] - meanf * a;
+  if (has_c) {
+    const float a = rstd * gam;
+    const float b = bet - meanf * a;
     float A = a, B = b;
     if (p.emb) {
-      const float sc = 1.0f + p.emb[(size_t)n * p.emb_stride + p.emb_off + c];
-      const float sh2 = p.emb[(size_t)n * p.emb_stride + p.emb_off + C + c];
+      const float sc = 1.0f + esc;
       A = a * sc;
-      B = b * sc + sh2;
+      B = b * sc + esh;
     }
-    p.A[(size_t)n * C + c] = A;
-    p.B[(size_t)n * C + c] = B;
+    p.A[(size_t)n * C + cc] = A;
+    p.B[(size_t)n * C + cc] = B;
   }
 }
 
@@ -381,6 +393,7 @@ int launch_gn_finalize2(const float* part0, int E0, float cnt0, int C0, const fl
   fp.emb = emb; fp.emb_stride = emb_stride; fp.emb_off = emb_off;
   fp.eps = 1e-5f;
   fp.A = A; fp.B = B;
+  IFD_REQUIRE((C0 + C1) % GN_G == 0 && (C0 + C1) / GN_G <= GN_NT, "GroupNorm group width");
   hipLaunchKernelGGL(gn_finalize2_kernel, dim3(GN_G, N), dim3(GN_NT), 0, stream, fp);
   return (int)hipGetLastError();
 }
