@@ -327,19 +327,46 @@ __global__ __launch_bounds__(256) void wgrad9_kernel(WgArgs a) {
 // unaligned: it ran no faster than the fp32 wgrad9_kernel; the loads and the unaligned reads each
 // cost more than the MFMAs.)
 #ifndef WX_ABL
-#define WX_ABL 0  // development timing ablations: 2 no global loads after the first chunk
+#define WX_ABL 0  // development timing ablations (outputs garbage): 2 no global loads after the first chunk,
+                  // 3 no staging (split + LDS writes) after the first chunk, 4 no MFMAs, 5 no fragment
+                  // reads after each chunk's first
 #endif
 constexpr int WX_PX = 64;                 // output pixels per chunk
 constexpr int WX_HMAX = 136;              // halo pixels: 4 x 34, 6 x 18, 10 x 10
-constexpr int WX_D = 2 * WX_PX * 64;      // f16 per stage: dY, both parts
-constexpr int WX_X = 2 * WX_HMAX * 64;    // X halo, both parts
+// LDS rows (one pixel's 64 channels) at a pitch of 96 f16 = 192 B = 48 banks: any 4 consecutive rows
+// start 48 r mod 64 = {0, 48, 32, 16} banks apart, so a transposed read's 4 rows x 64 B cover all 64 banks
+// whatever its first row - a tap's shift is then a plain row offset (an immediate or one add), not a
+// per-read swizzle (the XOR-swizzled 64-f16 rows of round 2 cost ~5 VALU per fragment read)
+constexpr int WX_P = 96;
+constexpr int WX_OOB = 0x7ffffff0;  // a buffer offset past mkrsrc's range: the load returns zeros
+constexpr int WX_D = 2 * WX_PX * WX_P;    // f16 per stage: dY, both parts
+constexpr int WX_X = 2 * WX_HMAX * WX_P;  // X halo, both parts
+static_assert(2 * (WX_D + WX_X) * 2 <= 160 * 1024, "two stages fit the LDS");
 typedef _Float16 wx_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 wx_h4 __attribute__((ext_vector_type(4)));
 typedef unsigned wx_u2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) wx_u2 wx_lds_u2;
 
+#if WX_ABL == 4
+#define WX_MFMA(a, b, c, x, y, z) ([&]() { asm volatile("" ::"v"(a), "v"(b)); return (c); }())
+#else
+#define WX_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
+#endif
+// The split of two values (conv_x3.hip's split2): hi = f16 RNE of both by one v_cvt_pk_f16_f32, lo =
+// f16(v - hi) by v_fma_mix{lo,hi}_f16 reading hi's halves as f16 (v - hi is exact in fp32, rounded once);
+// the empty asm keeps v an fp32 register value (no folding of its producer into the conversion)
+__device__ __forceinline__ void wx_split2(float v0, float v1, unsigned& h, unsigned& l) {
+  asm volatile("" : "+v"(v0), "+v"(v1));
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  h = __builtin_bit_cast(unsigned, __builtin_convertvector(f2_t{v0, v1}, h2_t));
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(l)
+      : "v"(v0), "v"(v1), "v"(h));
+}
 // element offset of channel c (multiple of 4) of row r: 16-B chunk (c / 8) XOR 4 (bit 1 of r)
-__device__ __forceinline__ int wx_off(int r, int c) { return r * 64 + ((((c >> 3) ^ ((r & 2) << 1))) << 3) + (c & 7); }
+__device__ __forceinline__ int wx_off(int r, int c) { return r * WX_P + c; }
 
 typedef __fp16 wx_hv4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
 __device__ __forceinline__ wx_h4 wx_tr(const _Float16* L, int off) {
@@ -369,7 +396,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
   constexpr int NT = Cf::NT, WX_DI = Cf::DI, WX_XI = Cf::XI, NTMAX = Cf::NTMAX;
   constexpr int HALO = TAPS == 9 ? 1 : 0;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
-  __shared__ f32x4 csred[NT];
+  f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop (its last barrier)
   const int cin = a.c0;
   const int nci = (cin + 63) / 64;
   const int cit = blockIdx.x % nci, cot = blockIdx.x / nci;
@@ -397,13 +424,20 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
     // staging items: (pixel i >> 4, channel quad i & 15), i = tid + NT k; quad fixed per thread
     const int cq = tid & 15;
     const bool co_ok = co0 + 4 * cq + 3 < a.cout, ci_ok = ci0 + 4 * cq + 3 < cin;
-    f32x4 dv[WX_DI], xv[WX_XI];
-    int xhy[WX_XI], xhx[WX_XI];
+    // two register sets (chunk parity): a chunk's loads go out two chunks before its staging
+    f32x4 dvs[2][WX_DI], xvs[2][WX_XI];
+    int xhy[WX_XI], xhx[WX_XI], ld_x[WX_XI], ld_d[WX_DI];
 #pragma unroll
     for (int k = 0; k < WX_XI; ++k) {
       const int hp = (tid + NT * k) >> 4;
       xhy[k] = hp < HP ? hp / HWc - HALO : -1000000;  // halo row / column relative to the chunk origin
       xhx[k] = hp % HWc - HALO;
+      ld_x[k] = hp < HP ? ((xhy[k] * a.W + xhx[k]) * cin + ci0 + 4 * cq) * 4 : 0;  // bytes from the chunk origin
+    }
+#pragma unroll
+    for (int k = 0; k < WX_DI; ++k) {
+      const int m = (tid + NT * k) >> 4;
+      ld_d[k] = (((m >> lwc) * a.W + (m & (Wc - 1))) * a.cout + co0 + 4 * cq) * 4;
     }
     auto chunk_origin = [&](int64_t c, int& n, int& y0, int& x0) {
       const int64_t per_img = (int64_t)rows_per_img * segs;
@@ -412,29 +446,33 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       y0 = (rem / segs) * R;
       x0 = (rem % segs) * Wc;
     };
-    auto load = [&](int64_t c) {
+    auto load = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
+      f32x4(&dv)[WX_DI] = dvs[decltype(SETc)::value];
+      f32x4(&xv)[WX_XI] = xvs[decltype(SETc)::value];
       if (WX_ABL == 2 && c != c_beg) return;
       int n, y0, x0;
       chunk_origin(c, n, y0, x0);
-      const int64_t img = (int64_t)n * a.H;
+      // buffer loads from the chunk's image (SGPR descriptors, one add per load for the chunk origin);
+      // a padding / out-of-tile lane reads at an offset past the descriptor's range, which returns zeros
+      const rsrc_t rd = mkrsrc(a.dy + (size_t)n * a.H * a.W * a.cout);
+      const rsrc_t rx = mkrsrc(a.x0 + (size_t)n * a.H * a.W * cin);
+      const int od = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * a.cout * 4);
+      const int ox = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * cin * 4);
 #pragma unroll
-      for (int k = 0; k < WX_DI; ++k) {
-        const int m = (tid + NT * k) >> 4;
-        const int64_t pix = (img + y0 + (m >> lwc)) * a.W + x0 + (m & (Wc - 1));
-        dv[k] = co_ok ? *reinterpret_cast<const f32x4*>(a.dy + pix * a.cout + co0 + 4 * cq) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      for (int k = 0; k < WX_DI; ++k) dv[k] = bld4(rd, co_ok ? ld_d[k] + od : WX_OOB, 0);
 #pragma unroll
       for (int k = 0; k < WX_XI; ++k) {
         const int y = y0 + xhy[k], x = x0 + xhx[k];
-        const bool ok = ci_ok && y >= 0 && y < a.H && x >= 0 && x < a.W;
-        xv[k] = ok ? *reinterpret_cast<const f32x4*>(a.x0 + ((img + y) * a.W + x) * cin + ci0 + 4 * cq)
-                   : f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool ok = ci_ok && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W;
+        xv[k] = bld4(rx, ok ? ld_x[k] + ox : WX_OOB, 0);
       }
     };
     // staging of one chunk in WX_PARTS slices (items: the WX_DI dY quads, then the WX_XI halo quads), so
     // that chunk c + 1's split and LDS writes run between chunk c's k-steps
     constexpr int WX_ITEMS = WX_DI + WX_XI, WX_PARTS = WX_PX / 16, WX_PER = (WX_ITEMS + WX_PARTS - 1) / WX_PARTS;
-    auto store_part = [&](_Float16* L, int part) {
+    auto store_part = [&](_Float16* L, int part, auto SETc) __attribute__((always_inline)) {
+      const f32x4(&dv)[WX_DI] = dvs[decltype(SETc)::value];
+      const f32x4(&xv)[WX_XI] = xvs[decltype(SETc)::value];
       _Float16* X = L + WX_D;
 #pragma unroll
       for (int it = 0; it < WX_ITEMS; ++it) {
@@ -445,23 +483,18 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
         const int row = (tid + NT * k) >> 4;
         if (!isd && row >= HP) continue;
         if (isd && do_cs) csum += v;
-        wx_h4 hi, lo;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float x = v[j];
-          asm volatile("" : "+v"(x));
-          const _Float16 hh = (_Float16)x;
-          hi[j] = hh;
-          lo[j] = (_Float16)(x - (float)hh);
-          gmax = fmaxf(gmax, fabsf(x));
-        }
+        unsigned h0, l0, h1, l1;
+        wx_split2(v[0], v[1], h0, l0);
+        wx_split2(v[2], v[3], h1, l1);
+        const wx_u2 hi = {h0, h1}, lo = {l0, l1};
+        gmax = fmaxf(gmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
         const int o = wx_off(row, 4 * cq);
         if (isd) {
-          *(wx_lds_u2*)(L + o) = __builtin_bit_cast(wx_u2, hi);
-          *(wx_lds_u2*)(L + WX_PX * 64 + o) = __builtin_bit_cast(wx_u2, lo);
+          *(wx_lds_u2*)(L + o) = hi;
+          *(wx_lds_u2*)(L + WX_PX * WX_P + o) = lo;
         } else {
-          *(wx_lds_u2*)(X + o) = __builtin_bit_cast(wx_u2, hi);
-          *(wx_lds_u2*)(X + WX_HMAX * 64 + o) = __builtin_bit_cast(wx_u2, lo);
+          *(wx_lds_u2*)(X + o) = hi;
+          *(wx_lds_u2*)(X + WX_HMAX * WX_P + o) = lo;
         }
       }
     };
@@ -471,7 +504,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
     const int cA = wr + 16 * (G & 1) + pcol, cB = wc + 16 * (G & 1) + pcol;
     // MFMAs of one staged chunk for taps T0 .. T0 + NTAP - 1 into acc[0 .. NTAP - 1] (compile-time, so the
     // accumulators stay registers; the two tap groups are two copies of this code, selected per wave)
-    auto mfma_chunk = [&](auto T0c, auto NTc, const _Float16* L, _Float16* Ln, bool nxt) __attribute__((always_inline)) {
+    auto mfma_chunk = [&](auto T0c, auto NTc, const _Float16* L, _Float16* Ln, bool nxt, auto SETc) __attribute__((always_inline)) {
       constexpr int T0 = decltype(T0c)::value, NTAP = decltype(NTc)::value;
       // the lane's row / column roles laundered per chunk: the fragment addresses are then computed next
       // to their reads instead of ~80 of them being hoisted out of the chunk loop into registers (the
@@ -479,25 +512,31 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       int cAl = cA, cBl = cB, ql = q, hl = h;
       asm volatile("" : "+v"(cAl), "+v"(cBl), "+v"(ql), "+v"(hl));
       const _Float16* Dh = L;
-      const _Float16* Dl = L + WX_PX * 64;
       const _Float16* Xh = L + WX_D;
-      const _Float16* Xl = Xh + WX_HMAX * 64;
       // Software-pipelined: taps in pairs whose MFMAs alternate (no back-to-back accumulator
       // dependence), the next pair's B fragments read after the current pair's first MFMAs, the
       // next k-step's A fragments during the last pair (a read the MFMA waits on costs its latency).
+      // Fragment addresses = a per-chunk lane base + a wave-uniform row offset + immediates (the 4-row
+      // step, the lo plane). A: the k-step's pixels 16 st + 8 hl + (0..7) of the chunk. B: their halo
+      // pixels, (16 st + 8 hl) -> halo pixel hb = row (m0 >> lwc) x HWc + column (m0 & (Wc - 1)); for
+      // Wc >= 16 the lane half only moves the column (8 hl), for Wc = 8 it moves the row (hl HWc); the
+      // tap adds (t / 3) HWc + t % 3.
+      const _Float16* pA = Dh + (8 * hl + ql) * WX_P + cAl;
+      const _Float16* pB = Xh + ((Wc >= 16 ? 8 * hl : hl * HWc) + ql) * WX_P + cBl;
       auto fetchA = [&](int st, wx_h8& ahi, wx_h8& alo) {
-        const int m0 = 16 * st + 8 * hl;
-        const int oa0 = wx_off(m0 + ql, cAl), oa1 = wx_off(m0 + 4 + ql, cAl);
-        const wx_h4 ah0 = wx_tr(Dh, oa0), ah1 = wx_tr(Dh, oa1), al0 = wx_tr(Dl, oa0), al1 = wx_tr(Dl, oa1);
+        const _Float16* b = pA + 16 * st * WX_P;
+        const wx_h4 ah0 = wx_tr(b, 0), ah1 = wx_tr(b, 4 * WX_P), al0 = wx_tr(b, WX_PX * WX_P),
+                    al1 = wx_tr(b, WX_PX * WX_P + 4 * WX_P);
         ahi = wx_h8{ah0[0], ah0[1], ah0[2], ah0[3], ah1[0], ah1[1], ah1[2], ah1[3]};
         alo = wx_h8{al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
       };
       auto fetchB = [&](int st, int t, wx_h8& bhi, wx_h8& blo) {
-        const int m0 = 16 * st + 8 * hl;  // this lane-half's 8 pixels of the k-step: one row segment
-        const int hb = (m0 >> lwc) * HWc + (m0 & (Wc - 1));
+        const int m0 = 16 * st;  // (wave-uniform part of the k-step's first pixel)
+        const int hb = Wc >= 16 ? (m0 >> lwc) * HWc + (m0 & (Wc - 1)) : 2 * st * HWc;
         const int r0 = TAPS == 9 ? hb + (t / 3) * HWc + (t % 3) : hb;
-        const int ob0 = wx_off(r0 + ql, cBl), ob1 = wx_off(r0 + 4 + ql, cBl);
-        const wx_h4 bh0 = wx_tr(Xh, ob0), bh1 = wx_tr(Xh, ob1), bl0 = wx_tr(Xl, ob0), bl1 = wx_tr(Xl, ob1);
+        const _Float16* b = pB + __builtin_amdgcn_readfirstlane(r0 * WX_P);
+        const wx_h4 bh0 = wx_tr(b, 0), bh1 = wx_tr(b, 4 * WX_P), bl0 = wx_tr(b, WX_HMAX * WX_P),
+                    bl1 = wx_tr(b, WX_HMAX * WX_P + 4 * WX_P);
         bhi = wx_h8{bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
         blo = wx_h8{bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
       };
@@ -512,24 +551,26 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
         for (int pp = 0; pp < NPAIR; ++pp) {
           const int l0 = 2 * pp, l1 = 2 * pp + 1;  // local tap indices (accumulators)
           const bool two = l1 < NTAP;
-          acc[l0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b0h, acc[l0], 0, 0, 0);
-          if (two) acc[l1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b1h, acc[l1], 0, 0, 0);
+          acc[l0] = WX_MFMA(ahi, b0h, acc[l0], 0, 0, 0);
+          if (two) acc[l1] = WX_MFMA(ahi, b1h, acc[l1], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
           // next pair (or the next k-step's first pair, and its A fragments)
           wx_h8 n0h, n0l, n1h, n1l, nah, nal;
           const bool last = pp + 1 == NPAIR;
           const int nst = last ? st + 1 : st, nl0 = last ? 0 : l0 + 2;
           const bool more = nst < NST;
-          if (more) {
+          if (more && WX_ABL != 5) {
             fetchB(nst, T0 + nl0, n0h, n0l);
             if (nl0 + 1 < NTAP) fetchB(nst, T0 + nl0 + 1, n1h, n1l);
             if (last) fetchA(nst, nah, nal);
+          } else if (more) {
+            n0h = b0h; n0l = b0l; n1h = b1h; n1l = b1l; nah = ahi; nal = alo;
           }
           __builtin_amdgcn_sched_barrier(0);
-          acc[l0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b0l, acc[l0], 0, 0, 0);
-          if (two) acc[l1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, b1l, acc[l1], 0, 0, 0);
-          acc[l0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b0h, acc[l0], 0, 0, 0);
-          if (two) acc[l1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, b1h, acc[l1], 0, 0, 0);
+          acc[l0] = WX_MFMA(ahi, b0l, acc[l0], 0, 0, 0);
+          if (two) acc[l1] = WX_MFMA(ahi, b1l, acc[l1], 0, 0, 0);
+          acc[l0] = WX_MFMA(alo, b0h, acc[l0], 0, 0, 0);
+          if (two) acc[l1] = WX_MFMA(alo, b1h, acc[l1], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
           if (more) {
             b0h = n0h; b0l = n0l;
@@ -537,28 +578,38 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
             if (last) { ahi = nah; alo = nal; }
           }
         }
-        if (nxt) store_part(Ln, st);  // (block-uniform)
+        if (nxt && WX_ABL != 3) store_part(Ln, st, SETc);  // (block-uniform)
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    // prologue: chunk c_beg staged, chunk c_beg + 1 in flight. Iteration c: MFMAs of chunk c from
-    // lds[c & 1] with chunk c + 1's staging slices between its k-steps into lds[(c + 1) & 1] (read by
-    // chunk c - 1, whose MFMAs every wave finished before the previous barrier), then chunk c + 2's loads
-    load(c_beg);
+    // prologue: chunk c_beg staged, chunks c_beg + 1 (register set 1) and c_beg + 2 (set 0) in flight.
+    // Iteration c (k = c - c_beg): MFMAs of chunk c from lds[c & 1] with chunk c + 1's staging slices
+    // (set (k + 1) & 1) between its k-steps into lds[(c + 1) & 1] (read by chunk c - 1, whose MFMAs every
+    // wave finished before the previous barrier), then chunk c + 3's loads into the set just staged
+    // (round 3: one set, loads one chunk ahead, waited on after the chunk's first k-step: 2.36 ms for the
+    // 256^2 128 -> 128 layer at B = 32 vs 1.77 ms with the loads ablated)
+    const std::integral_constant<int, 0> set0;
+    const std::integral_constant<int, 1> set1;
+    load(c_beg, set0);
 #pragma unroll
-    for (int part = 0; part < WX_PARTS; ++part) store_part(lds[c_beg & 1], part);
+    for (int part = 0; part < WX_PARTS; ++part) store_part(lds[c_beg & 1], part, set0);
     __syncthreads();
-    if (c_beg + 1 < c_end) load(c_beg + 1);
-    for (int64_t c = c_beg; c < c_end; ++c) {
+    if (c_beg + 1 < c_end) load(c_beg + 1, set1);
+    if (c_beg + 2 < c_end) load(c_beg + 2, set0);
+    auto iter = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
       _Float16* L = lds[c & 1];
       _Float16* Ln = lds[(c + 1) & 1];
       const bool nxt = c + 1 < c_end;
       if (TAPS == 9 && grp == 1)
-        mfma_chunk(std::integral_constant<int, 5>(), std::integral_constant<int, 4>(), L, Ln, nxt);
+        mfma_chunk(std::integral_constant<int, 5>(), std::integral_constant<int, 4>(), L, Ln, nxt, SETc);
       else
-        mfma_chunk(std::integral_constant<int, 0>(), std::integral_constant<int, TAPS == 9 ? 5 : 1>(), L, Ln, nxt);
-      if (c + 2 < c_end) load(c + 2);
+        mfma_chunk(std::integral_constant<int, 0>(), std::integral_constant<int, TAPS == 9 ? 5 : 1>(), L, Ln, nxt, SETc);
+      if (c + 3 < c_end) load(c + 3, SETc);
       __syncthreads();
+    };
+    for (int64_t c = c_beg; c < c_end; c += 2) {
+      iter(c, set1);
+      if (c + 1 < c_end) iter(c + 1, set0);
     }
   }
   if (gmax >= 65504.0f) atomicOr(guard, 1u);
