@@ -399,7 +399,16 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
   f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop (its last barrier)
   const int cin = a.c0;
   const int nci = (cin + 63) / 64;
-  const int cit = blockIdx.x % nci, cot = blockIdx.x / nci;
+  // (channel tile, pixel split z) of this block. Workgroups go to the 8 XCDs round-robin in launch order;
+  // when the split count allows, the tiles of one z (the same dY rows and X halos) are put on one XCD so
+  // the second co / ci tile re-reads them from that XCD's L2 instead of HBM
+  int tile = blockIdx.x, zs = blockIdx.y;
+  if ((gridDim.y & 7) == 0) {
+    const int L = blockIdx.x + blockIdx.y * gridDim.x, j = L >> 3;
+    tile = j % gridDim.x;
+    zs = (j / gridDim.x) * 8 + (L & 7);
+  }
+  const int cit = tile % nci, cot = tile / nci;
   const int co0 = cot * 64, ci0 = cit * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5;
@@ -410,7 +419,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
   const int lwc = __builtin_ctz(Wc);
   const int segs = a.W / Wc, rows_per_img = a.H / R;
   const int64_t nch = (int64_t)a.N * rows_per_img * segs;
-  const int64_t c_beg = (int64_t)blockIdx.y * a.chunks_per_split;
+  const int64_t c_beg = (int64_t)zs * a.chunks_per_split;
   const int64_t c_end = c_beg + a.chunks_per_split < nch ? c_beg + a.chunks_per_split : nch;
   f32x16 acc[NTMAX];
 #pragma unroll
@@ -439,12 +448,14 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       const int m = (tid + NT * k) >> 4;
       ld_d[k] = (((m >> lwc) * a.W + (m & (Wc - 1))) * a.cout + co0 + 4 * cq) * 4;
     }
+    // (every count here is a power of two: H, W and the chunk shape are; shifts, no 64-bit division)
+    const int lpi = __builtin_ctz(rows_per_img * segs), lsg = __builtin_ctz(segs);
     auto chunk_origin = [&](int64_t c, int& n, int& y0, int& x0) {
-      const int64_t per_img = (int64_t)rows_per_img * segs;
-      n = (int)(c / per_img);
-      const int rem = (int)(c - (int64_t)n * per_img);
-      y0 = (rem / segs) * R;
-      x0 = (rem % segs) * Wc;
+      const int ci = (int)c;
+      n = ci >> lpi;
+      const int rem = ci & ((1 << lpi) - 1);
+      y0 = (rem >> lsg) * R;
+      x0 = (rem & (segs - 1)) * Wc;
     };
     auto load = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
       f32x4(&dv)[WX_DI] = dvs[decltype(SETc)::value];
@@ -463,7 +474,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
 #pragma unroll
       for (int k = 0; k < WX_XI; ++k) {
         const int y = y0 + xhy[k], x = x0 + xhx[k];
-        const bool ok = ci_ok && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W;
+        const bool ok = ci_ok & ((unsigned)y < (unsigned)a.H) & ((unsigned)x < (unsigned)a.W);  // (no branches)
         xv[k] = bld4(rx, ok ? ld_x[k] + ox : WX_OOB, 0);
       }
     };
@@ -594,8 +605,11 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
 #pragma unroll
     for (int part = 0; part < WX_PARTS; ++part) store_part(lds[c_beg & 1], part, set0);
     __syncthreads();
-    if (c_beg + 1 < c_end) load(c_beg + 1, set1);
-    if (c_beg + 2 < c_end) load(c_beg + 2, set0);
+    // (loads past the block's range re-read its last chunk: every iteration issues the same loads, so
+    // the compiler's vmcnt arithmetic waits for one set only - a conditional load made it wait for both)
+    auto clampc = [&](int64_t c) { return c < c_end ? c : c_end - 1; };
+    load(clampc(c_beg + 1), set1);
+    load(clampc(c_beg + 2), set0);
     auto iter = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
       _Float16* L = lds[c & 1];
       _Float16* Ln = lds[(c + 1) & 1];
@@ -604,7 +618,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
         mfma_chunk(std::integral_constant<int, 5>(), std::integral_constant<int, 4>(), L, Ln, nxt, SETc);
       else
         mfma_chunk(std::integral_constant<int, 0>(), std::integral_constant<int, TAPS == 9 ? 5 : 1>(), L, Ln, nxt, SETc);
-      if (c + 3 < c_end) load(c + 3, SETc);
+      load(clampc(c + 3), SETc);
       __syncthreads();
     };
     for (int64_t c = c_beg; c < c_end; c += 2) {
@@ -622,12 +636,12 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int co = co0 + 4 * tid + j;
-        if (co < a.cout) colpart[(size_t)blockIdx.y * a.cout + co] = t[j];
+        if (co < a.cout) colpart[(size_t)zs * a.cout + co] = t[j];
       }
     }
   }
   // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin][TAPS]
-  float* slab = a.part + (size_t)blockIdx.y * a.cout * cin * TAPS;
+  float* slab = a.part + (size_t)zs * a.cout * cin * TAPS;
   const int ci = ci0 + wc + (lane & 31);
   const int tbase = TAPS == 9 ? 5 * grp : 0, ntap = TAPS == 9 ? (grp ? 4 : 5) : 1;
 #pragma unroll
