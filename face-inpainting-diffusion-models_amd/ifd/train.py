@@ -493,7 +493,14 @@ class UNetTrainer:
         hc = so["x"].shape[-1]
         co = dout6.shape[-1]  # the head's channel count padded to 4 (zero gradient in the pad)
         self.wgrad(dout6, co, so["a"], hc, N, H, "out.2.weight", "out.2.bias")
-        da = self.conv(dout6, co, N, H, "out.2.weight", transpose=True)
+        if self._x3_active(True) and co % 16:
+            # the split kernel's dgrad reads 16-channel chunks: the head gradient padded with zero channels
+            # (else the 8-channel dgrad runs on the fp32 kernel, ~4x the split kernel's time at 256^2)
+            d16 = self._zeros(N, H, H, 16)
+            self.copy_ch(dout6, co, 0, d16, 16, 0, co, N * H * H, False)
+            da = self.conv(d16, 16, N, H, "out.2.weight", transpose=True)
+        else:
+            da = self.conv(dout6, co, N, H, "out.2.weight", transpose=True)
         dh = self.gn_bwd(da, so["x"], N, H * H, hc, "out.0.", so["stats"], silu=True)
         # hs gradients from the output blocks' skip inputs
         in_blocks = [b for b in self.plan if b[0] == "input"]
