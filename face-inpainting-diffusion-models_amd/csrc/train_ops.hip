@@ -326,6 +326,9 @@ __global__ __launch_bounds__(256) void wgrad9_kernel(WgArgs a) {
 // (A first version staged both operands transposed through dword loads and read the shifted X rows
 // unaligned: it ran no faster than the fp32 wgrad9_kernel; the loads and the unaligned reads each
 // cost more than the MFMAs.)
+#ifndef WX_IL
+#define WX_IL 1  // staging items interleaved with the MFMA pairs (0: one slice after each k-step)
+#endif
 #ifndef WX_ABL
 #define WX_ABL 0  // development timing ablations (outputs garbage): 2 no global loads after the first chunk,
                   // 3 no staging (split + LDS writes) after the first chunk, 4 no MFMAs, 5 no fragment
@@ -481,18 +484,17 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
     // staging of one chunk in WX_PARTS slices (items: the WX_DI dY quads, then the WX_XI halo quads), so
     // that chunk c + 1's split and LDS writes run between chunk c's k-steps
     constexpr int WX_ITEMS = WX_DI + WX_XI, WX_PARTS = WX_PX / 16, WX_PER = (WX_ITEMS + WX_PARTS - 1) / WX_PARTS;
-    auto store_part = [&](_Float16* L, int part, auto SETc) __attribute__((always_inline)) {
+    auto store_item = [&](_Float16* L, int it, auto SETc) __attribute__((always_inline)) {
       const f32x4(&dv)[WX_DI] = dvs[decltype(SETc)::value];
       const f32x4(&xv)[WX_XI] = xvs[decltype(SETc)::value];
       _Float16* X = L + WX_D;
-#pragma unroll
-      for (int it = 0; it < WX_ITEMS; ++it) {
-        if (it / WX_PER != part) continue;
+      {
+        if (it >= WX_ITEMS) return;
         const bool isd = it < WX_DI;
         const int k = isd ? it : it - WX_DI;
         const f32x4 v = isd ? dv[k] : xv[k];
         const int row = (tid + NT * k) >> 4;
-        if (!isd && row >= HP) continue;
+        if (!isd && row >= HP) return;
         if (isd && do_cs) csum += v;
         unsigned h0, l0, h1, l1;
         wx_split2(v[0], v[1], h0, l0);
@@ -508,6 +510,10 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
           *(wx_lds_u2*)(X + WX_HMAX * WX_P + o) = lo;
         }
       }
+    };
+    auto store_part = [&](_Float16* L, int part, auto SETc) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < WX_PER; ++q) store_item(L, part * WX_PER + q, SETc);
     };
     // transposed-read lane roles: group G = lane >> 4 (G & 1: which 16 of the wave's 32 columns, G >> 1 = h:
     // which 8 of the k-step's 16 pixels); lane 4q + p of the group addresses row q, columns 4p .. 4p + 3
@@ -578,6 +584,11 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
             n0h = b0h; n0l = b0l; n1h = b1h; n1l = b1l; nah = ahi; nal = alo;
           }
           __builtin_amdgcn_sched_barrier(0);
+          // chunk c + 1's staging, one item per pair, beside this pair's second MFMA group
+          // (the last pair takes the part's remaining items: the 1x1 kernel has one pair per k-step)
+          if (WX_IL && nxt && WX_ABL != 3)  // (block-uniform)
+#pragma unroll
+            for (int q = pp; q < (pp + 1 == NPAIR ? WX_PER : pp + 1); ++q) store_item(Ln, st * WX_PER + q, SETc);
           acc[l0] = WX_MFMA(ahi, b0l, acc[l0], 0, 0, 0);
           if (two) acc[l1] = WX_MFMA(ahi, b1l, acc[l1], 0, 0, 0);
           acc[l0] = WX_MFMA(alo, b0h, acc[l0], 0, 0, 0);
@@ -589,7 +600,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
             if (last) { ahi = nah; alo = nal; }
           }
         }
-        if (nxt && WX_ABL != 3) store_part(Ln, st, SETc);  // (block-uniform)
+        if (!WX_IL && nxt && WX_ABL != 3) store_part(Ln, st, SETc);  // (block-uniform)
         __builtin_amdgcn_sched_barrier(0);
       }
     };
