@@ -317,12 +317,11 @@ __global__ __launch_bounds__(256) void wgrad9_kernel(WgArgs a) {
 // (v_mfma_f32_32x32x16_f16, K = 16 output pixels). Per chunk of 64 output pixels (2 rows of 32, or
 // 64 / W whole rows) the block stages, pixel-major as they sit in HBM (16-B loads, no transpose):
 //   D [part][64 px][64 co]      X [part][halo px, row-major (R + 2) x (Wc + 2) <= 136][64 ci]   f16
-// and the MFMA operands, which want 8 consecutive pixels of one channel per lane, come from
-// ds_read_b64_tr_b16 (4 pixel rows x 16 channels per 16-lane group, delivered column-major): a tap's
-// shift only changes which halo rows a lane addresses. 16-B chunks of a row are XOR-swizzled by
-// bit 1 of the row, so the 4 rows x 64 B a 32-lane half reads cover all 64 banks once. Double-
-// buffered; wave w owns the 32 x 32 quadrant (co 32 (w & 1), ci 32 (w >> 1)) of all 9 taps (144
-// accumulator registers). dY carries the backward's loss scale; |v| >= 65504 sets the range guard.
+// (one row per pixel at a 96-f16 pitch, WX_P below) and the MFMA operands, which want 8 consecutive
+// pixels of one channel per lane, come from ds_read_b64_tr_b16 (4 pixel rows x 16 channels per
+// 16-lane group, delivered column-major): a tap's shift only changes which halo rows a lane
+// addresses. Double-buffered; the waves' quadrants and tap groups are described at WxCfg. dY carries
+// the backward's loss scale; |v| >= 65504 sets the range guard.
 // (A first version staged both operands transposed through dword loads and read the shifted X rows
 // unaligned: it ran no faster than the fp32 wgrad9_kernel; the loads and the unaligned reads each
 // cost more than the MFMAs.)
@@ -368,7 +367,7 @@ __device__ __forceinline__ void wx_split2(float v0, float v1, unsigned& h, unsig
       : "=&v"(l)
       : "v"(v0), "v"(v1), "v"(h));
 }
-// element offset of channel c (multiple of 4) of row r: 16-B chunk (c / 8) XOR 4 (bit 1 of r)
+// element offset of channel c of row r
 __device__ __forceinline__ int wx_off(int r, int c) { return r * WX_P + c; }
 
 typedef __fp16 wx_hv4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
@@ -1958,7 +1957,9 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
                          int64_t colpart_floats, unsigned* guard, void* stream) {
   // the split kernel: 3x3 or 1x1, one input tensor, power-of-two maps >= 8, channel counts in 16-B quads
   // (its staging loads four channels at a time); else fp32
-  if ((taps != 9 && taps != 1) || c1 || H < 8 || (H & (H - 1)) || !guard || cout % 4 || c0 % 4)
+  // (and images within a buffer descriptor's 2 GB range: the staging loads address one image each)
+  if ((taps != 9 && taps != 1) || c1 || H < 8 || (H & (H - 1)) || !guard || cout % 4 || c0 % 4 ||
+      (int64_t)H * H * (cout > c0 ? cout : c0) * 4 >= 0x7ffffff0)
     return ifd_tr_conv_wgrad(dy, cout, x0, c0, x1, c1, N, H, taps, dw, db, part, part_floats, colpart, colpart_floats,
                              stream);
   const int64_t P = (int64_t)N * H * H;
