@@ -499,7 +499,10 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
         wx_split2(v[0], v[1], h0, l0);
         wx_split2(v[2], v[3], h1, l1);
         const wx_u2 hi = {h0, h1}, lo = {l0, l1};
-        gmax = fmaxf(gmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        // (v_max3 with |.| modifiers: two values per instruction)
+        asm("v_max3_f32 %0, %0, |%1|, |%2|\n\tv_max3_f32 %0, %0, |%3|, |%4|"
+            : "+v"(gmax)
+            : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
         const int o = wx_off(row, 4 * cq);
         if (isd) {
           *(wx_lds_u2*)(L + o) = hi;
