@@ -89,7 +89,9 @@ __global__ __launch_bounds__(256) void skinny_kernel(const float* __restrict__ i
 #pragma unroll
     for (int q = 0; q < SK_NB; ++q) acc[q] = 0.f;
     if (j < J) {
-#pragma unroll 4
+      // (16 weight loads in flight per wave: the loop is latency-bound at ~1 wave per SIMD; the
+      // accumulation order per slot is unchanged)
+#pragma unroll 16
       for (int kk = k0; kk < k0 + kc; ++kk) {
         const float w = wt[(size_t)kk * J + j];
         const f32x4* s4 = reinterpret_cast<const f32x4*>(sk + (size_t)kk * SK_NB);
