@@ -15,6 +15,7 @@ and keeps the rank's rows (results independent of the GPU count, at
 generating N x the rank's noise on-device); the default `device` mode draws per rank (per-rank seeds).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--noise device|parity]
+    python bench.py --workload c4 --gpus 8      # configs[3]: 512 images sharded 8 ways (64 per GPU)
 """
 from __future__ import annotations
 
@@ -119,14 +120,30 @@ def pmc_traffic(kernel):
     return {"traffic": None}
 
 
-def parallelism_note(ws):
+def distinct_devices(dev):
+    """Number of distinct GPUs the ranks ran on: every rank contributes (hostname, PCI domain:bus:device or
+    UUID) and the unique entries are counted, so multi-node jobs and launchers that give each rank one
+    visible device are counted right (the local torch.cuda.device_count() sees only this process's
+    devices)."""
+    import socket
+    import torch.distributed as dist
+    pr = torch.cuda.get_device_properties(dev)
+    uid = str(getattr(pr, "uuid", "")) or f"{pr.pci_domain_id}:{pr.pci_bus_id}:{pr.pci_device_id}"
+    key = (socket.gethostname(), uid)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return 1
+    keys = [None] * dist.get_world_size()
+    dist.all_gather_object(keys, key)
+    return len(set(keys))
+
+
+def parallelism_note(ws, ndev):
     """The parallel layout as it really ran: backend and distinct devices. Fewer GPUs than ranks (ranks
     sharing a device over gloo) is a rehearsal of the N-rank path, not an N-GPU measurement."""
     if ws == 1:
         return "dp1 (one GPU)"
     import torch.distributed as dist
     backend = dist.get_backend() if dist.is_initialized() else "none"
-    ndev = min(ws, torch.cuda.device_count())
     note = f"dp{ws} (image shards over {ndev} device(s), {backend} all_gather of outputs)"
     if ndev < ws:
         note += " REHEARSAL: ranks share devices, not an N-GPU result"
@@ -302,8 +319,13 @@ def main():
                     help="N=1 only: also time this many steps in the reduced-precision f16 mode, reported separately "
                          "(the reference's .half() experiment, code/test_quant.py:390-409; 0 = skip)")
     ap.add_argument("--ddpm-steps", type=int, default=1000, help="--workload ddpm: diffusion steps T (linear)")
-    ap.add_argument("--workload", choices=["sample", "train", "ddpm"], default="sample",
-                    help="sample: the headline DDIM-100 sampler (default); train: the training step (configs[4]); ddpm: DDPM-1000 at B=64 (configs[2])")
+    ap.add_argument("--workload", choices=["sample", "c4", "train", "ddpm"], default="sample",
+                    help="sample: the headline DDIM-100 sampler, --batch images per GPU (default; configs[1]); c4: the "
+                         "same loop over a fixed global batch of 512 sharded over the ranks (configs[3]); train: the "
+                         "training step (configs[4]); ddpm: DDPM-1000 at B=64 (configs[2])")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="sample / c4: total images over all ranks, sharded contiguously (sizes differ by at most "
+                         "one; default --batch x ranks, or 512 for c4)")
     ap.add_argument("--noise", choices=["device", "parity"], default="device",
                     help="device: per-rank GPU RNG (throughput); parity: full-batch device draws in reference order, "
                          "sliced per rank (GPU-count-independent results)")
@@ -329,17 +351,23 @@ def main():
     dev = parallel.device_for(local)
     torch.cuda.set_device(dev)
     parallel.init(device=dev)
-    B, H = args.batch, FULL.image_size
+    ndev = distinct_devices(dev)
+    H = FULL.image_size
+    c4 = args.workload == "c4"
+    G = args.global_batch or (512 if c4 else args.batch * ws)  # the job's images (configs[3]: 512 over 8 GPUs)
+    lo, hi = parallel.shard_range(G, rank, ws)
+    B = hi - lo  # this rank's images
+    if B < 1:
+        raise SystemExit(f"bench: global batch {G} leaves rank {rank} of {ws} without images")
 
     model = DiffusionInpaintingModel(FULL, device=dev, precision=args.precision)
     model.load_state_dict(make_state_dict(FULL, seed=1))
     model.eval()
     diffusion = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="cosine")
     if args.noise == "parity":
-        lo, hi = parallel.shard_range(B * ws, rank, ws)
         sampler = InpaintingSampler(model, diffusion, ddim_timesteps=args.ddim_steps, device=dev,
-                                    noise_shard=(lo, hi, B * ws))
-        gt, mask = (v[lo:hi].contiguous() for v in synth_inputs(B * ws, H, seed=7, device=dev))
+                                    noise_shard=(lo, hi, G))
+        gt, mask = (v[lo:hi].contiguous() for v in synth_inputs(G, H, seed=7, device=dev))
     else:
         sampler = InpaintingSampler(model, diffusion, ddim_timesteps=args.ddim_steps, device=dev)
         gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
@@ -353,7 +381,7 @@ def main():
         with torch.no_grad():
             y = sampler.inpainting_ddim_sample_loop(sampler.model_fn, shape, gt, mask, True, dev, False, args.eta)
             y = sampler.final_blend(y, gt, mask)
-            return parallel.gather_images(y, B * ws)
+            return parallel.gather_images(y, G)
 
     prof = not args.no_profile
     import ctypes
@@ -417,18 +445,19 @@ def main():
         roofline["all_conv_launches"] = {"achieved": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),
                                          "time_share": round(conv_ms / tot_ms, 4)}
 
-    value = B * ws * args.steps / elapsed
+    value = G * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     res = {
         "metric": "256x256 DDIM-100 inpainted images/sec at 1/2/4/8 MI355X; per-step UNet ms",
         "value": round(value, 4),
         "unit": "images/s",
-        "n_gpus": min(ws, torch.cuda.device_count()),
+        "n_gpus": ndev,
         "n_ranks": ws,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2),
         "unet_ms_per_eval": round(ms_per_step / n_evals, 3),
+        "unet_ms_per_eval_note": "per UNet eval of the largest rank's shard (the slowest rank sets the time)",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value * README_S_PER_SAMPLE_DDIM100, 2),
@@ -436,19 +465,24 @@ def main():
         "dtype": "f32" if args.precision == "fp32" else "f32 (3xf16 split MFMA, fp32 accumulate)",
         "precision": {"mode": args.precision,
                       "note": ("exact fp32 MFMA (an fp32 fma chain)" if args.precision == "fp32" else
-                               "each fp32 operand = f16 hi + f16 lo; 3 f16 MFMA products per MAC into one fp32 "
-                               "accumulator; error vs an fp64 UNet equals fp32's (tests/test_cpu_split_numerics.py) "
-                               "and every GPU parity test holds at the fp32 tolerances (tests/test_gpu_x3.py)")},
+                               "each fp32 operand = f16 hi + f16 lo; 3 exact f16 MFMA products per MAC, hi x hi into "
+                               "one fp32 accumulator and the two correction products into a second, added once per "
+                               "output; error vs an fp64 UNet within ~1.2x of the reference's own fp32 error "
+                               "(tests/test_gpu_full.py::test_c1_eval_error_vs_fp64, tools/diag/acc_model.py)")},
         "data": "synthetic (gt~U(-1,1), centre-square + rectangle masks, seeded random-init weights)",
         "noise": args.noise,
-        "config": {"workload": "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1])",
-                   "global_batch": B * ws, "batch_per_gpu": B, "unet_evals_per_image": n_evals,
+        "config": {"workload": ("C4: CelebA-HQ-shaped 256x256, global batch sharded over the ranks, DDIM-100 cosine "
+                                "T=1000 eta=0.75, all_gather of the outputs (BASELINE configs[3])" if c4 else
+                                "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1])"),
+                   "global_batch": G, "batch_per_gpu": B if G % ws == 0 else f"{G // ws}-{-(-G // ws)}",
+                   "unet_evals_per_image": n_evals,
                    "gflop_per_unet_eval_per_image": round(gflop_per_image(FULL), 2),
-                   "parallelism": parallelism_note(ws)},
+                   "parallelism": parallelism_note(ws, ndev)},
         "roofline": roofline,
         "cpu_baseline": None,
     }
-    if ws == 1 and args.precision != "fp32" and args.fp32_exact_steps > 0:
+    extras = ws == 1 and not c4  # the other arithmetic modes are timed beside the headline at N = 1 only
+    if extras and args.precision != "fp32" and args.fp32_exact_steps > 0:
         # the same workload in exact-fp32 mode, timed separately (same inputs, same clocked region)
         model.precision = "fp32"
         one_pass(0)
@@ -462,7 +496,7 @@ def main():
         res["fp32_exact"] = {"value": round(B * args.fp32_exact_steps / el32, 4), "unit": "images/s",
                              "ms_per_step": round(el32 / args.fp32_exact_steps * 1e3, 2),
                              "steps": args.fp32_exact_steps, "warmup": 1, "dtype": "f32"}
-    if ws == 1 and args.precision == "3xf16" and args.f16_steps > 0:
+    if extras and args.precision == "3xf16" and args.f16_steps > 0:
         # the reduced-precision variant (not fp32-class), same workload, timed separately
         model.precision = "f16"
         one_pass(0)
@@ -477,15 +511,16 @@ def main():
                               "ms_per_step": round(el16 / args.f16_steps * 1e3, 2), "steps": args.f16_steps,
                               "warmup": 1, "dtype": "f16 operands, fp32 accumulate (not fp32-class; "
                                                     "tests/test_gpu_f16.py records its error)"}
-    if rank == 0 and ws == 1 and args.cpu_baseline_seconds > 0:
-        res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
-    if rank == 0:
-        if kernels:
-            res["kernels"] = {k: {"count": int(v["count"]), "ms": round(v["ms"], 3)} for k, v in kernels.items()}
-        print(json.dumps(res), flush=True)
-    if parallel.world()[1] > 1:
+    if rank == 0 and kernels:
+        res["kernels"] = {k: {"count": int(v["count"]), "ms": round(v["ms"], 3)} for k, v in kernels.items()}
+    # the process group goes first: no rank then waits inside a collective while rank 0 times the CPU path
+    if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if rank == 0:
+        if args.cpu_baseline_seconds > 0:  # on this node's host cores, at any N, after the timed region
+            res["cpu_baseline"] = cpu_baseline(args.cpu_baseline_seconds)
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -83,8 +83,8 @@ struct ConvParams {
   // handle options (read once at ifd_create, ifd_set_option): development overrides and the
   // batch-invariant geometry (split-K and tile kind chosen per image, not per batch, so an image's
   // result does not depend on how many other images share the launch)
-  int opt_bm128, opt_lds_pad, opt_stream_cw, opt_invariant;
-  int opt_x3_order;  // split kernel unit order: 0 auto, 1 XCD-concurrent channel tiles, 2 = 1 for skip layers only
+  int opt_bm128;  // fp32 kernel: 128-pixel tiles only (the training 1x1 convs)
+  int opt_invariant;
   // 3xf16 range guard (conv_x3.hip): set to 1 when an operand's magnitude reaches the f16 range
   // (|a| >= 65504 would split into inf). The host re-runs the eval in fp32 when it is set.
   unsigned* guard;
@@ -107,11 +107,6 @@ int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t str
 // 3xf16 split-precision streaming kernel (conv_x3.hip); wpack = the x3 packing (pack_conv_x3).
 bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn);
 int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream);
-// Wide-unit variant (conv_x3w.hip): 8 x 16 pixels x 128 output channels per unit, weights from L2
-// straight into the MFMA waves' registers; wpack = pack_conv_x3 with BN = 128.
-void conv_x3w_geometry(ConvParams& p, int H, int W, int N);
-bool conv_x3w_eligible(const ConvParams& p, int taps, int xform);
-int launch_conv_x3w(const ConvParams& p, int xform, hipStream_t stream);
 
 // A ResBlock's 1x1 skip_connection on split f16 MFMAs as its own launch (skip_x3.hip):
 // out = bias + W * cat(s0, s1) per pixel, NHWC fp32 in and out; conv2 then adds it as its residual.

@@ -530,8 +530,7 @@ static int launch_one(const ConvParams& p, hipStream_t stream) {
   const int npA = NP > BM ? NP : BM;
   const size_t stage = (size_t)(2 * npA * 8 + 2 * 9 * 8 * BN);
   const size_t epi = (size_t)BM * (BN + 4);  // NHWC epilogue tile (the final-conv tile is smaller)
-  const size_t pad = (size_t)p.opt_lds_pad;  // development option: force 1 block / CU
-  const size_t lds = (stage > epi ? stage : epi) * sizeof(float) + pad;
+  const size_t lds = (stage > epi ? stage : epi) * sizeof(float);
   const bool one = p.IMGS == 1;
   if constexpr (BM == 256) {  // only used for W >= 32 (one image per tile, 2*NP <= 1024)
     if (!one || 2 * NP > 4 * NP_T) return (int)hipErrorInvalidValue;
@@ -556,7 +555,7 @@ int conv_pick_bn(int cout, int taps, int H, int W, int N) {
 // the grid still gives >= 2 blocks per CU: it halves the weight-slab loads per MFMA, the producer's
 // bottleneck. Otherwise BM = 128, with split-K to cover the chip on the low-resolution layers.
 void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool x3) {
-  const bool allow256 = !p.opt_bm128;  // development option: 128-pixel tiles only
+  const bool allow256 = !p.opt_bm128;  // (the training 1x1 convs: 256-pixel tiles are instantiated for 3x3 only)
   int bm = 128;
   if (x3) {
     // 3xf16 split kernel (conv_x3.hip): 256-pixel tiles of one image (8 x 32 or 16 x 16) whatever

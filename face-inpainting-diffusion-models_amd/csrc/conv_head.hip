@@ -295,9 +295,9 @@ __global__ __launch_bounds__(256, 2) void conv_head_x3_kernel(ConvParams p, cons
   if (nwork > 0) load(blockIdx.x, 0);
   for (int u = 0; u < nwork; ++u) {
     const int t = blockIdx.x + u * gridDim.x;
-    hx_f4 acc[4];
+    hx_f4 acc[4], accl[4];  // hi x hi products; the two correction products (added once per output)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = hx_f4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) acc[r] = accl[r] = hx_f4{0.f, 0.f, 0.f, 0.f};
     for (int c = 0; c < nch; ++c) {
       __syncthreads();  // previous chunk's MFMA reads (and the weight copy) done
       stage(t);
@@ -329,8 +329,8 @@ __global__ __launch_bounds__(256, 2) void conv_head_x3_kernel(ConvParams p, cons
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bh, acc[r], 0, 0, 0);
-            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bl, acc[r], 0, 0, 0);
-            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[r + ky], bh, acc[r], 0, 0, 0);
+            accl[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bl, accl[r], 0, 0, 0);
+            accl[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[r + ky], bh, accl[r], 0, 0, 0);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void conv_head_x3_kernel(ConvParams p, cons
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Ob[((4 * wave + r) * HX_T + 4 * kg + e) * 8 + li] = acc[r][e] * (1.0f / 2048.0f);
+        for (int e = 0; e < 4; ++e) Ob[((4 * wave + r) * HX_T + 4 * kg + e) * 8 + li] = (acc[r][e] + accl[r][e]) * (1.0f / 2048.0f);
     __syncthreads();
     {
       int n, y0, x0;

@@ -626,9 +626,8 @@ int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t str
     if (xform == XF_UP) return launch_stream2_inst<XF_UP>(p, stream);
     return (int)hipErrorInvalidValue;
   }
-  const bool cw4 = p.opt_stream_cw == 4;  // development option: 4 or 8 consumer waves
-  if (xform == XF_NONE) return cw4 ? launch_stream_inst<XF_NONE, 4>(p, stream) : launch_stream_inst<XF_NONE, 8>(p, stream);
-  if (xform == XF_UP) return cw4 ? launch_stream_inst<XF_UP, 4>(p, stream) : launch_stream_inst<XF_UP, 8>(p, stream);
+  if (xform == XF_NONE) return launch_stream_inst<XF_NONE, 8>(p, stream);
+  if (xform == XF_UP) return launch_stream_inst<XF_UP, 8>(p, stream);
   return (int)hipErrorInvalidValue;  // avg-pool prologue: conv.hip (its 4-source register sets do not fit 3 deep)
 }
 

@@ -131,10 +131,9 @@ struct XDec {
 };
 __device__ __forceinline__ XDec x3_dec(const ConvParams& p, int nct) {
   const bool pow2 = (nct & (nct - 1)) == 0;
-  const bool order_ok = p.opt_x3_order == 0 || (p.opt_x3_order == 2 && !p.wskip);
   return {__builtin_ctz(p.ksplit), __builtin_ctz(nct), __builtin_ctz(p.tiles_x), __builtin_ctz(p.tiles_y),
           __builtin_ctz(p.IMGS), pow2 && p.npix_tiles % 8 == 0,
-          order_ok && p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0, nct, pow2};
+          p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0, nct, pow2};
 }
 // Unit u of block b. blk_major (no split-K, pixel tiles a multiple of the grid): block b takes
 // pixel tiles b, b + G, ... and runs all channel tiles of each back to back, so the second
@@ -399,27 +398,38 @@ __device__ __forceinline__ f32x16 xmfma(f16x8 a, f16x8 b, f32x16 c) {
 // operand = the halo stage (planes of Geo::NP pixels, pb = halo pixel).
 // NPROD = 1 (the f16 precision mode): the hi x hi product only.
 template <int TW, int NPROD>
-__device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As, const lds_f* Ws, const int (&pb)[2]) {
+__device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], f32x16 (&accl)[2][2], const lds_f* As, const lds_f* Ws,
+                                           const int (&pb)[2]) {
   using Geo = XGeo<TW>;
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const lds_f* Ah = As + 4 * (h * Geo::NP);
   const lds_f* Al = As + 4 * ((2 + h) * Geo::NP);
   const lds_f* Wb = Ws + 4 * (h * XBN + l32);
-  f16x8 ah[2][2], al[2][2], bs[2][2], bl[2][2];
-  auto fetch = [&](int tap, int slot) {
-    const int toff = (tap / 3) * Geo::HW + (tap % 3);
+  // hi fragments double-buffered (the next tap's are read right after the current tap's first MFMA
+  // group); lo fragments single-buffered, each re-read as soon as the group that uses it is issued,
+  // eight MFMAs before its next use (16 registers fewer: the residual prefetch fits beside both
+  // accumulator sets' successors)
+  f16x8 ah[2][2], bs[2][2], al[2], bl[2];
+  auto toff = [&](int tap) { return (tap / 3) * Geo::HW + (tap % 3); };
+  auto fetch_hi = [&](int tap, int slot) {
 #pragma unroll
-    for (int mr = 0; mr < 2; ++mr) {
-      ah[slot][mr] = *(const lds_h8*)(Ah + 4 * (pb[mr] + toff));
-      if (NPROD == 3) al[slot][mr] = *(const lds_h8*)(Al + 4 * (pb[mr] + toff));
-    }
+    for (int mr = 0; mr < 2; ++mr) ah[slot][mr] = *(const lds_h8*)(Ah + 4 * (pb[mr] + toff(tap)));
 #pragma unroll
-    for (int nr = 0; nr < 2; ++nr) {
-      bs[slot][nr] = *(const lds_h8*)(Wb + 4 * (tap * 4 * XBN + nr * 32));
-      if (NPROD == 3) bl[slot][nr] = *(const lds_h8*)(Wb + 4 * (tap * 4 * XBN + 2 * XBN + nr * 32));
-    }
+    for (int nr = 0; nr < 2; ++nr) bs[slot][nr] = *(const lds_h8*)(Wb + 4 * (tap * 4 * XBN + nr * 32));
   };
-  fetch(0, 0);
+  auto fetch_bl = [&](int tap) {
+#pragma unroll
+    for (int nr = 0; nr < 2; ++nr) bl[nr] = *(const lds_h8*)(Wb + 4 * (tap * 4 * XBN + 2 * XBN + nr * 32));
+  };
+  auto fetch_al = [&](int tap) {
+#pragma unroll
+    for (int mr = 0; mr < 2; ++mr) al[mr] = *(const lds_h8*)(Al + 4 * (pb[mr] + toff(tap)));
+  };
+  fetch_hi(0, 0);
+  if (NPROD == 3) {
+    fetch_bl(0);
+    fetch_al(0);
+  }
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int cur = tap & 1;
@@ -429,19 +439,24 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], const lds_f* As,
       for (int nr = 0; nr < 2; ++nr)
         acc[mr][nr] = xmfma(ah[cur][mr], bs[cur][nr], acc[mr][nr]);
     __builtin_amdgcn_sched_barrier(0);
-    if (tap + 1 < 9) fetch(tap + 1, cur ^ 1);
+    if (tap + 1 < 9) fetch_hi(tap + 1, cur ^ 1);
     __builtin_amdgcn_sched_barrier(0);
     if (NPROD == 1) continue;
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr)
-        acc[mr][nr] = xmfma(ah[cur][mr], bl[cur][nr], acc[mr][nr]);
+        accl[mr][nr] = xmfma(ah[cur][mr], bl[nr], accl[mr][nr]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (tap + 1 < 9) fetch_bl(tap + 1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr)
-        acc[mr][nr] = xmfma(al[cur][mr], bs[cur][nr], acc[mr][nr]);
+        accl[mr][nr] = xmfma(al[mr], bs[cur][nr], accl[mr][nr]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (tap + 1 < 9) fetch_al(tap + 1);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -476,7 +491,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   if (consumer) {
     const int h = lane >> 5, l32 = lane & 31;
     const int wm0 = wave * 64;
-    f32x16 acc[2][2];
+    f32x16 acc[2][2], accl[2][2];  // hi x hi products; the two correction products (module comment)
     int pb[2];
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr) {
@@ -490,14 +505,19 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
 #pragma unroll
         for (int nr = 0; nr < 2; ++nr)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[mr][nr][r] = 0.f;
+          for (int r = 0; r < 16; ++r) {
+            acc[mr][nr][r] = 0.f;
+            accl[mr][nr][r] = 0.f;
+          }
     };
     // Epilogue straight from the accumulators. Lane (h, l32) holds channel 32 nr + l32 of tile
     // pixel wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3) (column offset 4 h + (r & 3) < 8 stays in
     // its row): one dword store per register = two 128-B row segments. Bias and residual are
     // loaded in the same layout while the unit's last chunk is on the MFMAs, so the epilogue
     // waits on nothing and its stores drain behind the next unit's chunks.
-    float rv[2][2][16];
+    // rv (the residual prefetch) is declared per unit, inside the unit loop: declared out here, a unit
+    // without a prefetch (split-K, no residual) would carry the previous unit's values, so the 64
+    // registers would be live through every chunk
     float bias2[2];
     // Register (mr, r) of lane (h, l32) sits at tile pixel wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3).
     // Byte offsets: vbase (lane: tile origin, the wave's rows, 4 h, channel) + mr * mstep (lane) +
@@ -514,7 +534,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     };
     // SKIP kernels have no residual (the host runs a 1x1 conv with a residual, proj_out, split-K: the
     // reduction adds it). Its 64 registers would not fit beside the skip operand buffers.
-    auto prefetch = [&](const STile& t) {
+    auto prefetch = [&](const STile& t, float (&rv)[2][2][16]) {
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr) bias2[nr] = gld1(p.bias + t.ct * XBN + 32 * nr + l32);
       if (SKIP || !p.res) return;
@@ -530,20 +550,25 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
               rv[mr][nr][r] = __builtin_bit_cast(
                   float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb + mr * mstep + nr * 128, roff(r), 0));
       } else {  // XF_UP: nearest-upsampled residual (XF_DOWN residuals arrive pre-pooled)
+        // tile pixel wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3): the first three terms are wave-uniform and a
+        // multiple of 8 (TW >= 8), so the source pixel's row is uniform and its column is a uniform part
+        // + 2 h + ((r & 3) >> 1): one lane base, the rest scalar offsets (per-register VGPR addresses
+        // spilled once the correction accumulators took their registers)
+        const int vb = (2 * h * p.cout + t.ct * XBN + l32) * 4;
 #pragma unroll
         for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
-          for (int nr = 0; nr < 2; ++nr)
+          for (int r = 0; r < 16; ++r) {
+            const int ub = wm0 + 32 * mr + 8 * (r >> 2);
+            const int y = (t.y0 + ub / TW) >> 1, x = ((t.x0 + ub % TW) >> 1) + ((r & 3) >> 1);
+            const int so = (y * p.res_W + x) * p.cout * 4;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int lin = wm0 + 32 * mr + 8 * (r >> 2) + 4 * h + (r & 3);
-              const int y = (t.y0 + lin / TW) >> 1, x = (t.x0 + lin % TW) >> 1;
-              const int o = ((y * p.res_W + x) * p.cout + t.ct * XBN + 32 * nr + l32) * 4;
-              rv[mr][nr][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, o, 0, 0));
-            }
+            for (int nr = 0; nr < 2; ++nr)
+              rv[mr][nr][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb + nr * 128, so, 0));
+          }
       }
     };
-    auto epilogue = [&](const STile& t, int z, bool tstamp = false) {
+    auto epilogue = [&](const STile& t, int z, const float (&rv)[2][2][16], bool tstamp = false) {
       if (X3_ABLATE == 13) {  // timing only: no epilogue
         asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
         return;
@@ -742,24 +767,44 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && j < 16)
         p.trace[64 * blockIdx.x + slot + j] = __builtin_amdgcn_s_memtime();
     };
-    zero();
     if (IFD_TRACE && p.trace && wave == 0 && lane == 0) p.trace[64 * blockIdx.x + 58] = __builtin_amdgcn_s_memtime();
     XBARRIER_CONSUMER();  // chunk 0 staged
     int j = 0;  // position in the block's chunk stream: ring slot j % 3, A stage j & 1
     for (int u = 0; u < nu; ++u) {
       int z;
       const STile t = unit_of(u, z);
+      float rv[2][2][16];
+      zero();  // (here, not after the epilogue: the zeros of the next unit are then not live through this one)
       // the unit's K range [c0, c1): 3x3 chunks [c0, me), then skip chunks [sb, se) of the 1x1 segment
       const int c0 = z * nchu, c1 = c0 + nchu;
       const int me = c1 < nmain ? c1 : nmain;
       const int sb = (c0 > nmain ? c0 : nmain) - nmain, se = c1 - nmain;
       const bool has_skip = SKIP && sb < se;
-      auto main_chunk = [&]() __attribute__((always_inline)) {
+      // sep: the correction products into accl; otherwise into acc (after fold)
+      auto main_chunk = [&](bool sep) __attribute__((always_inline)) {
         stamp(j);
-        if (X3_ABLATE != 4) consume_x3<TW, NPROD>(acc, A0 + (j & 1) * XA, W0 + (j % 3) * XW, pb);
+        if (X3_ABLATE != 4) {
+          if (sep)
+            consume_x3<TW, NPROD>(acc, accl, A0 + (j & 1) * XA, W0 + (j % 3) * XW, pb);
+          else
+            consume_x3<TW, NPROD>(acc, acc, A0 + (j & 1) * XA, W0 + (j % 3) * XW, pb);
+        }
         stamp(j, 16);
         ++j;
         XBARRIER_CONSUMER();
+      };
+      // the correction sum joins the main one (one rounding per output) before the unit's last 3x3
+      // chunk: from there on accl is dead and its registers hold the residual / skip-operand prefetch
+      auto fold = [&]() __attribute__((always_inline)) {
+        if (NPROD == 1) return;
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int nr = 0; nr < 2; ++nr) {
+            acc[mr][nr] += accl[mr][nr];
+            // pinned here: hipcc otherwise sinks the adds past the residual prefetch (both sets live)
+            asm volatile("" : "+v"(acc[mr][nr])::"memory");
+          }
       };
       // The unit's last 3x3 chunk is peeled: what it prefetches (residual, first skip operands) is then
       // not a loop-carried value. The two cases are separate branches so that the operand buffers are
@@ -767,19 +812,21 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       if (!has_skip) {
         // the residual / bias prefetch goes out X3_PREF chunks before the unit's end (peeled)
         constexpr int PF = X3_PREF;
-        for (int c = c0; c < me - PF; ++c) main_chunk();
+        for (int c = c0; c < me - PF; ++c) main_chunk(true);
         if (me > c0) {
-          if (!SKIP && S == 1) prefetch(t);
-          for (int c = (me - PF > c0 ? me - PF : c0); c < me; ++c) main_chunk();
+          fold();
+          if (!SKIP && S == 1) prefetch(t, rv);
+          for (int c = (me - PF > c0 ? me - PF : c0); c < me; ++c) main_chunk(false);
         }
       } else {
         skip_setup(t);
-        for (int c = c0; c < me - 1; ++c) main_chunk();
+        for (int c = c0; c < me - 1; ++c) main_chunk(true);
+        fold();
         // one definition point per operand buffer on every path (a buffer defined in two branches
         // gets register copies at the merge, and a copy of a load in flight is a vmcnt wait)
         const int sb1 = sb + 1 < se ? sb + 1 : sb;  // (a one-chunk segment reloads its chunk: harmless)
         skip_load_all(sq0, sb);                      // a whole 3x3 chunk ahead of its use
-        if (me > c0) main_chunk();
+        if (me > c0) main_chunk(false);
         skip_load_all(sq1, sb1);
         auto skip_step = [&](f32x4(&b)[2][XSL], bool reload, int next) __attribute__((always_inline)) {
           stamp(j);
@@ -803,15 +850,14 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           if (sk + 1 < se) skip_step(sq1, false, 0);
         }
       }
-      if (SKIP && S == 1) prefetch(t);  // (bias only: SKIP kernels have no residual)
+      if (SKIP && S == 1) prefetch(t, rv);  // (bias only: SKIP kernels have no residual)
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
         p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
-      epilogue(t, z, u == 0);
+      epilogue(t, z, rv, u == 0);
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0) {
         __builtin_amdgcn_s_waitcnt(0);  // (trace builds: wait for the stores to leave)
         p.trace[64 * blockIdx.x + 63] = __builtin_amdgcn_s_memtime();    // first epilogue: end
       }
-      zero();
     }
     if (SKIP && p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
     if (IFD_TRACE && p.trace && wave == 0 && lane == 0) {  // consumer done (stores issued)

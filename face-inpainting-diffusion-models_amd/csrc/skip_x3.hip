@@ -134,12 +134,15 @@ __global__ __launch_bounds__(SK_NT, SK_WPE) void skip_x3_kernel(Skip1x1Params p)
 #pragma unroll
   for (int nr = 0; nr < NR; ++nr) bias[nr] = gld1(p.bias + nt * NTC + 32 * nr + l32);
   float gmax = 0.f;
-  f32x16 acc[NR];
+  f32x16 acc[NR], accl[NR];  // hi x hi products; the two correction products (one rounding per output at the end)
   for (int t = w0; t < ntiles; t += GW) {
 #pragma unroll
     for (int nr = 0; nr < NR; ++nr)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[nr][r] = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        acc[nr][r] = 0.f;
+        accl[nr][r] = 0.f;
+      }
     for (int ks = 0; ks < KS; ks += SK_D) {
 #pragma unroll
       for (int d = 0; d < SK_D; ++d) {
@@ -178,9 +181,9 @@ __global__ __launch_bounds__(SK_NT, SK_WPE) void skip_x3_kernel(Skip1x1Params p)
         for (int nr = 0; nr < NR; ++nr) acc[nr] = mfma16(ah, bs[nr], acc[nr]);
         if (NPROD == 3) {
 #pragma unroll
-          for (int nr = 0; nr < NR; ++nr) acc[nr] = mfma16(ah, bl[nr], acc[nr]);
+          for (int nr = 0; nr < NR; ++nr) accl[nr] = mfma16(ah, bl[nr], accl[nr]);
 #pragma unroll
-          for (int nr = 0; nr < NR; ++nr) acc[nr] = mfma16(al, bs[nr], acc[nr]);
+          for (int nr = 0; nr < NR; ++nr) accl[nr] = mfma16(al, bs[nr], accl[nr]);
         }
       }
     }
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(SK_NT, SK_WPE) void skip_x3_kernel(Skip1x1Params p)
     for (int nr = 0; nr < NR; ++nr) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float x = acc[nr][r] * (1.0f / kScale) + bias[nr];
+        const float x = (acc[nr][r] + accl[nr][r]) * (1.0f / kScale) + bias[nr];
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + nr * 128,
                                               (8 * (r >> 2) + (r & 3)) * p.cout * 4, 0);
       }

@@ -1562,35 +1562,6 @@ __global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int c
   dst[((base + 2 + hh) * 64 + col) * 8 + j] = lo;
 }
 
-// the same split packing at BN = 128 for the wide-unit kernel (conv_x3w.hip, unet.hip x3w_off)
-__global__ void pack_conv_x3w_kernel(const float* __restrict__ w, int cout, int cin, int cin_pad16,
-                                     _Float16* __restrict__ dst, unsigned* guard) {
-#pragma clang fp contract(off)
-  const int nch = cin_pad16 / 16;
-  const int64_t tot = (int64_t)(cout / 128) * nch * 9 * 2 * 128 * 8;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= tot) return;
-  const int j = (int)(i & 7);
-  int64_t r = i >> 3;
-  const int col = (int)(r & 127);
-  r >>= 7;
-  const int hh = (int)(r & 1);
-  r >>= 1;
-  const int tap = (int)(r % 9);
-  r /= 9;
-  const int chk = (int)(r % nch);
-  const int ct = (int)(r / nch);
-  const int o = ct * 128 + col, c = chk * 16 + hh * 8 + j;
-  const float v = c < cin ? w[((size_t)o * cin + c) * 9 + tap] : 0.f;
-  const _Float16 hi = (_Float16)v;
-  const float s = (float)hi * 2048.0f;
-  if (!(fabsf(s) <= 65504.0f)) atomicOr(guard, 2u);
-  const _Float16 lo = (_Float16)((v - (float)hi) * 2048.0f);
-  const size_t base = ((((size_t)ct * nch + chk) * 9 + tap) * 2) * 2;  // part 0
-  dst[((base + hh) * 128 + col) * 8 + j] = (_Float16)s;
-  dst[((base + 2 + hh) * 128 + col) * 8 + j] = lo;
-}
-
 // 3xf16 packing of a 1x1 conv weight for the split kernel's 1x1 chunks (unet.hip pack_skip_x3's layout:
 // [cout_pad/64][cin/32][q][part][h][64][8] f16, element (q, part, h, col, j) of chunk s = split part of
 // W[64 ct + col][32 s + 16 h + 8 q + j]); transpose=1 packs the dgrad conv (out = cin, in = cout).
@@ -1834,59 +1805,6 @@ int ifd_tr_conv_x3_gstat(const float* x0, int c0, const float* x1, int c1, int N
                          int* gstat_E, float* gstat_cnt, void* stream) {
   return conv_x3_run(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, taps,
                      gstat, gstat_floats, gstat_E, gstat_cnt, stream);
-}
-
-int64_t ifd_tr_x3w_pack_bytes(int cout, int cin_pad16) { return (int64_t)cout * cin_pad16 * 9 * 4; }
-
-int ifd_tr_pack_conv_x3w(const float* w, int cout, int cin, int cin_pad16, void* wx3w, unsigned* guard, void* stream) {
-  if (!w || !wx3w || !guard || cin_pad16 % 16 || cout % 128 || cin > cin_pad16) {
-    set_error("ifd_tr_pack_conv_x3w: bad arguments");
-    return 2;
-  }
-  const int64_t tot = (int64_t)(cout / 128) * (cin_pad16 / 16) * 9 * 2 * 2 * 128 * 8;
-  hipLaunchKernelGGL(pack_conv_x3w_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, w, cout, cin, cin_pad16,
-                     (_Float16*)wx3w, guard);
-  return TR_LAST();
-}
-
-int ifd_tr_conv_x3w(const float* x0, int c0, const float* x1, int c1, int N, int H, int xform, const void* wx3w,
-                    const float* bias, int cin_pad, int cout, int act, const float* A, const float* B,
-                    const float* res, int res_up, float* out, unsigned* guard, float* gstat, int64_t gstat_floats,
-                    int* gstat_E, float* gstat_cnt, void* stream) {
-  if (gstat_E) *gstat_E = 0;
-  if ((H & (H - 1)) || c0 + c1 != cin_pad || !x0 || !out || !wx3w || !bias || !guard || act < 0 || act > 2 ||
-      (act && (!A || !B)) || xform < 0 || xform > 1) {
-    set_error("ifd_tr_conv_x3w: unsupported arguments");
-    return 2;
-  }
-  ConvParams p;
-  std::memset(&p, 0, sizeof(p));
-  p.in0 = x0; p.c0 = c0; p.in1 = c1 ? x1 : nullptr; p.c1 = c1;
-  p.N = N; p.H = p.W = H; p.Hin = p.Win = xform == XF_UP ? H / 2 : H;
-  p.act = act; p.actA = A; p.actB = B;
-  p.wpack = (const float*)wx3w; p.bias = bias;
-  p.cin_pad = cin_pad; p.cout = cout; p.cout_pad = cout;
-  p.res = res; p.res_xform = res_up ? XF_UP : XF_NONE; p.res_H = p.res_W = res_up ? H / 2 : H;
-  p.out = out;
-  p.epi = EPI_NHWC;
-  p.guard = guard;
-  p.x3_nprod = 3;
-  conv_x3w_geometry(p, H, H, N);
-  if (!conv_x3w_eligible(p, 9, xform)) {
-    set_error("ifd_tr_conv_x3w: shape not eligible for the wide-unit kernel");
-    return 3;
-  }
-  if (gstat && gstat_E && gstat_cnt && (int64_t)N * (cout / 4) * p.tiles_x * p.tiles_y * 2 <= gstat_floats) {
-    p.gstat = gstat;
-    p.gstat_E = p.tiles_x * p.tiles_y;
-  }
-  const int e = launch_conv_x3w(p, xform, (hipStream_t)stream);
-  if (!e && p.gstat) {
-    *gstat_E = p.gstat_E;
-    *gstat_cnt = 512.f;
-  }
-  if (e) set_error(std::string("ifd_tr_conv_x3w: ") + hipGetErrorString((hipError_t)e));
-  return e;
 }
 
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream) {

@@ -24,7 +24,6 @@ struct ConvW {
   // the skip segment as its own launch (skip_x3.hip) in the split modes: split 1x1 packing, the
   // conv's own bias and the skip bias apart (b_off holds their sum for the fused kernels)
   size_t sk_off = 0, bmain_off = 0, sbias_off = 0;
-  size_t x3w_off = 0;  // the split packing at BN = 128 for the wide-unit kernel (conv_x3w.hip), 0 if none
   int sk_ntc = 0;
   bool sk_ok = false;
   std::string wname, bname, swname, sbname;  // source parameter names
@@ -172,18 +171,10 @@ class Model {
   int opt_stream_ = 2;      // wide fp32 layers: 0 one tile per workgroup, 1/2 persistent (1 or 2 per CU)
   int opt_x3_off_ = 0;      // bisecting mask: 1 no 16x16 tiles, 2 no split-K, 4 no skip layers, 8 no 8x8, 16 no 1x1,
                             // 32 no split-MFMA output head
-  int opt_stream_cw_ = 8;   // conv_stream consumer waves (4 or 8)
-  int opt_bm128_ = 0;       // 128-pixel fp32 tiles only
-  int opt_lds_pad_ = 0;     // extra LDS bytes per fp32 conv block
   int opt_invariant_ = 0;   // batch-invariant geometry (results independent of the batch split)
-  int opt_x3_order_ = 0;    // split kernel unit order (ConvParams::opt_x3_order)
-  int opt_x3w_ = 0;         // split modes: wide-unit 3x3 kernel at resolutions >= this (0 off)
   int opt_skip_sep_ = 64;   // split modes: ResBlock skip_connection as its own launch at resolutions >= this (0 off)
   void fill_opts(ConvParams& p) const {
-    p.opt_x3_order = opt_x3_order_;
-    p.opt_bm128 = opt_bm128_;
-    p.opt_lds_pad = opt_lds_pad_;
-    p.opt_stream_cw = opt_stream_cw_;
+    p.opt_bm128 = 0;
     p.opt_invariant = opt_invariant_;
   }
   const float* pooled_raw_ = nullptr;  // tensor whose raw 2x2 pool sits in o_pool2_ (act_pool)

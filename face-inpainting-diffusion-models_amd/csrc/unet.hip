@@ -28,13 +28,8 @@ Model::Model(const ifd_config& cfg) : cfg_(cfg) {
   opt_stream_ = env_int("IFD_CONV_STREAM", 2);
   opt_x3_off_ = env_int("IFD_X3_OFF", 0);
   gn_fused_ = env_int("IFD_GN_FUSED", 1) != 0;
-  opt_stream_cw_ = env_int("IFD_STREAM_CW", 8);
-  opt_bm128_ = env_int("IFD_CONV_BM", 0) == 128;
-  opt_lds_pad_ = env_int("IFD_CONV_LDS_PAD", 0);
   opt_invariant_ = env_int("IFD_BATCH_INVARIANT", 0) != 0;
-  opt_x3_order_ = env_int("IFD_X3_ORDER", 0);
   opt_skip_sep_ = env_int("IFD_SKIP_SEP", 64);
-  opt_x3w_ = env_int("IFD_X3W", 0);
 }
 
 int Model::set_option(const std::string& key, int v) {
@@ -45,20 +40,6 @@ int Model::set_option(const std::string& key, int v) {
     opt_x3_off_ = v;
   } else if (key == "gn_fused") {
     gn_fused_ = v != 0;
-  } else if (key == "stream_cw") {
-    IFD_REQUIRE(v == 4 || v == 8, "stream_cw must be 4 or 8");
-    opt_stream_cw_ = v;
-  } else if (key == "conv_bm128") {
-    opt_bm128_ = v != 0;
-  } else if (key == "lds_pad") {
-    IFD_REQUIRE(v >= 0 && v <= 65536, "lds_pad out of range");
-    opt_lds_pad_ = v;
-  } else if (key == "x3_order") {
-    IFD_REQUIRE(v >= 0 && v <= 2, "x3_order must be 0, 1 or 2");
-    opt_x3_order_ = v;
-  } else if (key == "x3w") {
-    IFD_REQUIRE(v >= 0, "x3w must be >= 0");
-    opt_x3w_ = v;
   } else if (key == "skip_sep") {
     IFD_REQUIRE(v >= 0, "skip_sep must be >= 0");
     opt_skip_sep_ = v;
@@ -75,13 +56,8 @@ int Model::get_option(const std::string& key, int* v) const {
   if (key == "conv_stream") *v = opt_stream_;
   else if (key == "x3_off") *v = opt_x3_off_;
   else if (key == "gn_fused") *v = gn_fused_ ? 1 : 0;
-  else if (key == "stream_cw") *v = opt_stream_cw_;
-  else if (key == "conv_bm128") *v = opt_bm128_;
-  else if (key == "lds_pad") *v = opt_lds_pad_;
   else if (key == "batch_invariant") *v = opt_invariant_;
-  else if (key == "x3_order") *v = opt_x3_order_;
   else if (key == "skip_sep") *v = opt_skip_sep_;
-  else if (key == "x3w") *v = opt_x3w_;
   else IFD_REQUIRE(false, "unknown option " + key);
   return 0;
 }
@@ -503,9 +479,6 @@ int Model::finalize() {
     } else if (c.taps == 1 && c.bn == 64 && c.cin_pad % kSkipChunk == 0 && !c.has_skip) {
       c.x3s_off = reserve((size_t)c.cout_pad * c.cin_pad);  // a 1x1 conv runs as 1x1 chunks only
     }
-    c.x3w_off = 0;
-    if (c.x3_off && c.taps == 9 && c.cout % 128 == 0 && c.cout == c.cout_pad)
-      c.x3w_off = reserve((size_t)c.cout_pad * c.cin_pad * c.taps);
     c.sk_off = c.bmain_off = c.sbias_off = 0;
     c.sk_ntc = 0;
     if (c.has_skip && c.x3_off && c.cout == c.cout_pad) c.sk_ntc = skip_x3_ntc(c.cs_pad, c.cout);
@@ -554,8 +527,6 @@ int Model::finalize() {
     pack_conv(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob, c.w_off);
     c.x3_ok = c.x3_off && pack_conv_x3(host_[c.wname], c.cout, c.cin, c.taps, c.bn, c.cin_pad, c.cout_pad, blob,
                                        c.x3_off);
-    if (c.x3_ok && c.x3w_off)  // (same weights and range check as the BN = 64 packing)
-      (void)pack_conv_x3(host_[c.wname], c.cout, c.cin, c.taps, 128, c.cin_pad, c.cout_pad, blob, c.x3w_off);
     if (c.taps == 1 && c.x3s_off)
       c.x3_ok = pack_skip_x3(host_[c.wname], c.cout, c.cin, c.bn, c.cin_pad, c.cout_pad, blob, c.x3s_off);
     if (c.x3_ok && c.has_skip)
@@ -904,20 +875,9 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   const bool x3_masked = x3_masked_for(p);
   const bool use_x3 = split_ && cw.x3_ok && !x3_masked && conv_x3_eligible(p, cw.taps, xf, cw.bn);
   IFD_REQUIRE(use_x3 || p.cin_pad == cw.cin_pad, "1x1-only operand rewrite without the split kernel");
-  bool use_x3w = false;
   if (use_x3) {
     p.wpack = wblob_ + cw.x3_off;
     if (cw.has_skip) p.wskip = wblob_ + cw.x3s_off;
-    // the wide-unit kernel for the large layers with 128-multiple widths (conv_x3w.hip)
-    if (cw.x3w_off && !cw.has_skip && opt_x3w_ > 0 && H >= opt_x3w_ && !(x3_off & 64)) {
-      ConvParams q = p;
-      conv_x3w_geometry(q, H, H, N);
-      q.wpack = wblob_ + cw.x3w_off;
-      if (conv_x3w_eligible(q, cw.taps, xf)) {
-        p = q;
-        use_x3w = true;
-      }
-    }
   } else if (x3_geo) {  // not split-eligible after all: the fp32 kernels' own geometry
     conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8);
   }
@@ -934,7 +894,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     auto it = stat_area_.find(out);
     if (it != stat_area_.end()) {
       p.gstat = it->second;
-      p.gstat_E = p.tiles_x * p.tiles_y * (use_stream && !use_x3w ? 4 : 1);
+      p.gstat_E = p.tiles_x * p.tiles_y * (use_stream ? 4 : 1);
     }
   }
 #if IFD_TRACE
@@ -970,10 +930,8 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
                    (cw.has_skip ? pix * cw.cs : 0) + (res ? pix * cw.cout : 0));
     if (prof_layers_)
       snprintf(nm, sizeof(nm), "%s<%d,%d,%d,%d> r%d %d+%d->%d skip%d",
-               use_x3w ? "conv_x3w" : use_x3 ? "conv_x3" : (use_head ? "conv_head" : (use_stream ? "conv_stream" : "conv_kernel")), p.bm,
+               use_x3 ? "conv_x3" : (use_head ? "conv_head" : (use_stream ? "conv_stream" : "conv_kernel")), p.bm,
                cw.bn, cw.taps, xf, H, c0, c1, cw.cout, cw.has_skip ? cw.cs : 0);
-    else if (use_x3w)
-      snprintf(nm, sizeof(nm), "conv_x3w_kernel<%d,%d>", xf, p.x3_nprod);
     else if (use_x3)
       snprintf(nm, sizeof(nm), "conv_x3_kernel<%d,%s,%d,%d>", xf, cw.has_skip ? "true" : "false", p.TW, p.x3_nprod);
     else if (use_head_x3)
@@ -983,7 +941,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
     else if (use_stream && stream_mode == 2)  // template arguments as in the rocprof kernel name
       snprintf(nm, sizeof(nm), "conv_stream2_kernel<%d>", xf);
     else if (use_stream)
-      snprintf(nm, sizeof(nm), "conv_stream_kernel<%d,%d>", xf, opt_stream_cw_);
+      snprintf(nm, sizeof(nm), "conv_stream_kernel<%d,8>", xf);
     else  // (BM,BN,WGM,WGN,TAPS,XF)
       snprintf(nm, sizeof(nm), "conv_kernel<%d,%d,%s,%d,%d>", p.bm, cw.bn,
                (p.bm == 256 || cw.bn == 32) ? "4,1" : "2,2", cw.taps, xf);
@@ -991,14 +949,13 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   hipEvent_t e0;
   prof_begin(s, &e0, nm);
   if (use_head) p.ksplit = 1;
-  int e = use_x3w      ? launch_conv_x3w(p, xf, s)
-          : use_x3     ? launch_conv_x3(p, xf, s)
+  int e = use_x3       ? launch_conv_x3(p, xf, s)
           : use_head_x3 ? launch_conv_head_x3(p, wblob_ + cw.head_x3_off, s)
           : use_head   ? launch_conv_head(p, wblob_ + cw.head_off, s)
           : use_stream ? launch_conv_stream(p, xf, stream_mode, s)
                        : launch_conv(p, cw.taps, xf, cw.bn, s);
   if (p.gstat)
-    stat_[out] = StatRec{p.gstat, p.gstat_E, 4.0f * (use_x3w ? p.bm : use_stream ? 64 : p.bm), cw.cout};
+    stat_[out] = StatRec{p.gstat, p.gstat_E, 4.0f * (use_stream ? 64 : p.bm), cw.cout};
   else
     stat_.erase(out);
 #if IFD_TRACE

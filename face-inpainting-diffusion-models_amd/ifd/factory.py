@@ -11,12 +11,16 @@ Differences, all deliberate:
     bias default-initialised from the global torch RNG (U(+-1/sqrt(fan_in)), as nn.Conv2d does —
     the exact RNG stream of the reference's module construction is not reproduced).
   * `noise_schedule` / `steps` are keyword overrides (defaults = the reference factory's).
-  * `precision` selects the conv arithmetic ("3xf16": the split mode, DESIGN.md §3a, whose error
-    against exact arithmetic matches the reference's own fp32 — tests/test_gpu_full.py — and whose
-    range guard recomputes any out-of-range eval in fp32; "fp32": the plain fp32 MFMA chain);
-    default from the IFD_PRECISION environment variable, else "fp32" (the reference's own
-    arithmetic class, bit-comparable with earlier fp32 runs), so the reference's scripts can opt into
-    "3xf16" without edits. The active mode is logged (logger "ifd") when the model is created.
+  * `precision` selects the conv arithmetic: "3xf16" (the default) or "fp32"; the IFD_PRECISION
+    environment variable overrides the default, so the reference's scripts switch without edits. The
+    active mode is logged (logger "ifd") when the model is created.
+    Why 3xf16 is the default: it is the MORE accurate of the two against exact arithmetic. Its products
+    are exact and its hi x hi sums go into one fp32 accumulator while the correction products go into a
+    second one, so per UNet eval its error against an fp64 UNet is within ~1.2x of the
+    reference's own fp32 (oneDNN) error (tests/test_gpu_full.py::test_c1_eval_error_vs_fp64). "fp32" runs
+    v_mfma_f32_32x32x2_f32, an fp32 FMA chain over K = 9 Cin terms with one rounding per product: ~2.6x
+    the reference's error (tools/diag/acc_model.py reproduces both ratios on the CPU). Out-of-range
+    split operands trip the range guard and the eval is recomputed in fp32.
 """
 from __future__ import annotations
 
@@ -43,7 +47,7 @@ def _unwrap(ckpt):
 def create_model_and_diffusion(checkpoint_path, device, img_size=256, *, steps=1000, noise_schedule="quadratic",
                                model_channels=128, seed=1, precision=None):
     cfg = UNetConfig(image_size=img_size, model_channels=model_channels)
-    precision = precision or os.environ.get("IFD_PRECISION", "fp32")
+    precision = precision or os.environ.get("IFD_PRECISION", "3xf16")
     logging.getLogger("ifd").info("create_model_and_diffusion: conv arithmetic %s (IFD_PRECISION)", precision)
     model = DiffusionInpaintingModel(cfg, device=device, precision=precision)
     if checkpoint_path is None:

@@ -79,7 +79,7 @@ class Handle:
 class DiffusionInpaintingModel(torch.nn.Module):
     """9-channel inpainting UNet (code/unet.py:176-200) executed by libifd."""
 
-    def __init__(self, cfg: UNetConfig = FULL, device=None, precision: str = "fp32", options=None):
+    def __init__(self, cfg: UNetConfig = FULL, device=None, precision: str = "3xf16", options=None):
         super().__init__()
         self.cfg = cfg
         # handle options (include/ifd.h ifd_set_option), e.g. {"batch_invariant": 1}
@@ -199,6 +199,9 @@ class DiffusionInpaintingModel(torch.nn.Module):
                 yield
             finally:
                 self._deferred = None
+            # the scope's forwards may have been enqueued on other streams than `s`: wait for all of them
+            # before the guard word is read (ifd_guard_read orders only after the work on `s`)
+            torch.cuda.synchronize(dev)
             tripped = ctypes.c_int()
             _lib.check(L.ifd_guard_read(h.h, ctypes.byref(tripped), s))
             if tripped.value:

@@ -43,10 +43,6 @@ TRAIN_EXPORTS = {
                                    vp, vp, vp]),
     "ifd_tr_gn_fwd_gstat": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, i32, vp, i32, f32, vp, vp, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
-    "ifd_tr_x3w_pack_bytes": (i64, [i32, i32]),
-    "ifd_tr_pack_conv_x3w": (i32, [vp, i32, i32, i32, vp, vp, vp]),
-    "ifd_tr_conv_x3w": (i32, [vp, i32, vp, i32, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, i64,
-                              vp, vp, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
     "ifd_tr_conv_wgrad": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp]),
@@ -493,13 +489,16 @@ class UNetTrainer:
         hc = so["x"].shape[-1]
         co = dout6.shape[-1]  # the head's channel count padded to 4 (zero gradient in the pad)
         self.wgrad(dout6, co, so["a"], hc, N, H, "out.2.weight", "out.2.bias")
+        da = None
         if self._x3_active(True) and co % 16:
             # the split kernel's dgrad reads 16-channel chunks: the head gradient padded with zero channels
-            # (else the 8-channel dgrad runs on the fp32 kernel, ~4x the split kernel's time at 256^2)
+            # (else the 8-channel dgrad runs on the fp32 kernel, ~4x the split kernel's time at 256^2).
+            # Only the split kernel takes the padded operand: when the shape is not eligible (e.g.
+            # model_channels not a multiple of 64) the fp32 kernel runs on the unpadded gradient.
             d16 = self._zeros(N, H, H, 16)
             self.copy_ch(dout6, co, 0, d16, 16, 0, co, N * H * H, False)
-            da = self.conv(d16, 16, N, H, "out.2.weight", transpose=True)
-        else:
+            da = self._conv_x3(d16, 16, N, H, "out.2.weight", None, None, None, 0, True)
+        if da is None:
             da = self.conv(dout6, co, N, H, "out.2.weight", transpose=True)
         dh = self.gn_bwd(da, so["x"], N, H * H, hc, "out.0.", so["stats"], silu=True)
         # hs gradients from the output blocks' skip inputs

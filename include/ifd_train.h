@@ -62,17 +62,6 @@ int ifd_tr_conv_x3_gstat(const float* x0, int c0, const float* x1, int c1, int N
                          const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
                          int64_t part_floats, unsigned* guard, int taps, float* gstat, int64_t gstat_floats,
                          int* gstat_E, float* gstat_cnt, void* stream);
-/* The wide-unit split kernel (conv_x3w.hip: 8 x 16 pixels x 128 output channels per unit) on one 3x3 conv:
- * out = conv3x3(act(xform(cat(x0, x1)))) + bias [+ res], act(v) = silu(A v + B) (act 2), A v + B (act 1) or v
- * (act 0) with A, B [N][c0 + c1]; xform 0 identity or 1 nearest-up x2 (input at H / 2); res at H (res_up 0)
- * or H / 2 (res_up 1, nearest-up). wx3w = ifd_tr_pack_conv_x3w; cout % 128 == 0, H % 16 == 0. Optional
- * GroupNorm granule statistics as ifd_tr_conv_x3_gstat (E = H*H / 128 entries of 512 values). */
-int64_t ifd_tr_x3w_pack_bytes(int cout, int cin_pad16);
-int ifd_tr_pack_conv_x3w(const float* w, int cout, int cin, int cin_pad16, void* wx3w, unsigned* guard, void* stream);
-int ifd_tr_conv_x3w(const float* x0, int c0, const float* x1, int c1, int N, int H, int xform, const void* wx3w,
-                    const float* bias, int cin_pad, int cout, int act, const float* A, const float* B,
-                    const float* res, int res_up, float* out, unsigned* guard, float* gstat, int64_t gstat_floats,
-                    int* gstat_E, float* gstat_cnt, void* stream);
 /* x[i] *= s (the loss scale of the 3xf16 backward and its removal from the gradients). */
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream);
 /* dw[cout][c0+c1][taps] += sum_pixels dy (x) shifted concat(x0, x1); db[cout] += column sums of dy. */

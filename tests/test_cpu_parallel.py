@@ -40,21 +40,24 @@ def _worker(rank, ws, port, gb, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("gb", [16, 5])
-def test_gather_and_max_gloo(gb):
+@pytest.mark.parametrize("ws,gb", [(2, 16), (2, 5), (8, 512), (8, 17)])
+def test_gather_and_max_gloo(ws, gb):
+    """World sizes 2 and 8 (bench.py --workload c4: 512 images over 8 ranks; 17 over 8 = uneven shards of
+    3 and 2): every rank gets the whole batch in order, and the job time is the slowest rank's."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, gb, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, gb, q)) for r in range(ws)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=120) for _ in procs]
+    out = [q.get(timeout=180) for _ in procs]
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
+    assert sorted(r for r, _, _ in out) == list(range(ws))
     for rank, vals, t in out:
         assert vals == [float(i) for i in range(gb)]
-        assert t == 2.0
+        assert t == float(ws)
 
 
 def _noise_worker(rank, ws, port, gb, q):

@@ -2,8 +2,9 @@
 
   * C4's per-rank shard (configs[3]: B=512 over 8 GPUs = 64 images per rank, DDIM-100 cosine,
     eta 0.75; code/test_inp_ddim_100.py:470-576): the first steps of the fused DDIM loop at B=64,
-    256x256. With the batch-invariant geometry (the multi-GPU parity mode) images 0, 37 and 63 equal
-    their own B=1 runs bit for bit, the noise drawn for the full batch and sliced.
+    256x256, in both modes, and the whole 100-step trajectory in 3xf16 (finite, no range-guard trip).
+    With the batch-invariant geometry (the multi-GPU parity mode) images equal their own B=1 runs bit
+    for bit, the noise drawn for the full batch and sliced.
   * C5's batch (configs[4]: the training step at B=32, code/train_inpainting.py:15-79): the full-size
     3xf16 step against the fp32 step, the gates of test_gpu_train.py::test_train_x3_full_matches_fp32.
   * The timed B=16 bench geometry (default options: persistent split-kernel units, four-image 8x8
@@ -94,6 +95,42 @@ def test_c4_rank_shard_ddim100_b64(record, prec):
     wb, wsb = m.memory()
     record(f"c4_rank_shard_b64_ddim3/{prec}", slice_vs_b1_maxabs=max(diffs.values()), workspace_bytes=wsb,
            weight_bytes=wb)
+
+
+def test_c4_rank_shard_full_trajectory(record):
+    """C4 per rank, the WHOLE trajectory: B=64 at 256x256, all 100 DDIM steps (cosine, eta 0.75, the
+    sampler's own loop with device-side full-batch draws) + the final blend in 3xf16 (the default
+    arithmetic). The output is finite, the range guard never trips (late-trajectory activations are the
+    ones that could approach the f16 range), and images 0 and 63 equal their own B=1 runs bit for bit
+    (batch-invariant geometry; the B=1 runs draw the full batch's noise and keep their row)."""
+    from bench import synth_inputs
+    from ifd.sampler import InpaintingSampler
+    from ifd.schedules import create_gaussian_diffusion
+    B, H = 64, 256
+    gt, mask = synth_inputs(B, H, seed=7, device=DEV)
+    m = _model("3xf16", batch_invariant=1)
+    trips0 = m.guard_trips
+    diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="cosine")
+
+    def run(lo, hi, shard):
+        s = InpaintingSampler(m, diff, ddim_timesteps=100, device=DEV, noise_shard=(lo, hi, B) if shard else None)
+        torch.manual_seed(42)
+        with torch.no_grad():
+            y = s.inpainting_ddim_sample_loop(s.model_fn, (hi - lo, 3, H, H), gt[lo:hi].contiguous(),
+                                              mask[lo:hi].contiguous(), True, DEV, False, 0.75)
+            return s.final_blend(y, gt[lo:hi].contiguous(), mask[lo:hi].contiguous())
+    y = run(0, B, False)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    assert m.guard_trips == trips0
+    diffs = {}
+    for i in (0, 63):
+        y1 = run(i, i + 1, True)
+        diffs[i] = float((y1 - y[i:i + 1]).abs().max())
+        assert torch.equal(y1, y[i:i + 1]), (i, diffs[i])
+    assert m.guard_trips == trips0
+    record("c4_rank_shard_b64_ddim100_full/3xf16", slice_vs_b1_maxabs=max(diffs.values()),
+           out_absmax=float(y.abs().max()), guard_trips=m.guard_trips - trips0)
 
 
 def test_workspace_arena_matches_plan(record):

@@ -32,7 +32,7 @@ def maxabs(a, b):
 @pytest.fixture(scope="module")
 def red_model():
     from ifd.model import DiffusionInpaintingModel
-    m = DiffusionInpaintingModel(REDUCED, device=DEV)
+    m = DiffusionInpaintingModel(REDUCED, device=DEV, precision="fp32")
     m.load_state_dict(make_state_dict(REDUCED, seed=1))
     return m.eval()
 
@@ -40,7 +40,7 @@ def red_model():
 @pytest.fixture(scope="module")
 def full_model():
     from ifd.model import DiffusionInpaintingModel
-    m = DiffusionInpaintingModel(FULL, device=DEV)
+    m = DiffusionInpaintingModel(FULL, device=DEV, precision="fp32")
     m.load_state_dict(make_state_dict(FULL, seed=1))
     return m.eval()
 

@@ -181,3 +181,52 @@ def test_train_x3_range_guard():
     assert tr3.guard_trips == 1
     assert l3 == l32
     assert torch.equal(tr3.flat, p32)
+
+
+def test_train_x3_head_dgrad_fallback(record):
+    """The 3xf16 backward pads the head's 8-channel gradient to 16 channels for the split kernel's dgrad;
+    when the split kernel cannot take that conv (model_channels not a multiple of 64: simulated here by
+    making the split path decline it, since the fp32 trainer itself needs 64-multiples) the fp32 kernel must
+    run on the UNPADDED gradient (the padded operand there raised ValueError). The step then
+    matches the fp32 step from the same state (loss relative 1e-5, per-tensor gradients rel-L2 1e-4)."""
+    from bench import synth_inputs
+    from ifd.schedules import create_gaussian_diffusion
+    from ifd.train import UNetTrainer
+    cfg = REDUCED
+    diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="quadratic")
+    gt, mask = synth_inputs(2, cfg.image_size, seed=5, device=DEV)
+    res = {}
+    for prec, decline in (("fp32", False), ("3xf16", True)):
+        tr = UNetTrainer(cfg, device=DEV, precision=prec)
+        tr.load_state_dict(make_state_dict(cfg, seed=1))
+        declined = []
+        if decline:
+            orig = tr._conv_x3
+
+            def conv_x3(x, cin_x, N, H, name, bias_name, r, x1, c1, transpose, _orig=orig):
+                if name == "out.2.weight" and transpose:
+                    declined.append(cin_x)
+                    return None
+                return _orig(x, cin_x, N, H, name, bias_name, r, x1, c1, transpose)
+            tr._conv_x3 = conv_x3
+        torch.manual_seed(11)
+        t = torch.randint(0, 1000, (2,), device=DEV)
+        noise = torch.randn(2, 3, cfg.image_size, cfg.image_size, device=DEV)
+        torch.manual_seed(12)
+        loss = float(tr.train_step(diff, gt, gt * (1 - mask), mask, t, noise=noise))
+        torch.cuda.synchronize()
+        assert tr.guard_trips == 0
+        if decline:
+            assert declined == [16]  # the padded operand was offered, declined, and the fp32 path ran
+        res[prec] = (loss, tr.grad.clone(), tr.offsets)
+        del tr
+    (l32, g32, offs), (l3, g3, _) = res["fp32"], res["3xf16"]
+    worst = 0.0
+    for k, (o, shape) in offs.items():
+        n = int(np.prod(shape))
+        b = g32[o:o + n].double()
+        if float(b.norm()) > 0:
+            worst = max(worst, float((g3[o:o + n].double() - b).norm() / b.norm()))
+    record("train_x3_head_dgrad_fallback_vs_fp32", rel_loss=abs(l3 - l32) / abs(l32), max_tensor_grad_rel=worst)
+    assert abs(l3 - l32) <= 1e-5 * abs(l32)
+    assert worst <= 1e-4

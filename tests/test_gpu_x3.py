@@ -97,28 +97,6 @@ def test_x3_skip_launch(evals, x3_model, record, skip_sep):
     assert maxabs(y, y_def) <= 2e-5
 
 
-@pytest.mark.parametrize("x3w", [16, 64])
-def test_x3_wide_units(evals, x3_model, record, x3w):
-    """The wide-unit 3x3 kernel (conv_x3w_kernel: 8x16 pixels x 128 output channels per unit; option
-    x3w = the smallest resolution it runs at, off in the default plan) against the reference output
-    and against the default plan (every 3x3 layer on conv_x3_kernel)."""
-    from ifd.model import DiffusionInpaintingModel
-    x, gt, mask = (_t(evals[f"full/{k}"]).to(DEV) for k in ("x", "gt", "mask"))
-    t = torch.tensor([999], device=DEV)
-    m = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16", options={"x3w": x3w})
-    m.load_state_dict(make_state_dict(FULL, seed=1))
-    with torch.no_grad():
-        y_def, ks = _kernels_run(x3_model, lambda: x3_model(x, t, masked_image=gt * (1 - mask), mask=mask))
-        y, ks2 = _kernels_run(m, lambda: m(x, t, masked_image=gt * (1 - mask), mask=mask))
-    assert not any(k.startswith("conv_x3w") for k in ks), sorted(ks)
-    assert {"conv_x3w_kernel<0,3>", "conv_x3w_kernel<1,3>"} <= set(ks2), sorted(ks2)
-    ref = _t(evals["full_t999/y"])
-    e_def, e = maxabs(y_def, ref), maxabs(y, ref)
-    record(f"unet_full_t999/3xf16/x3w{x3w}", maxabs=e, maxabs_default_plan=e_def)
-    assert e_def <= 1e-5 and e <= 1e-5
-    assert maxabs(y, y_def) <= 2e-5
-
-
 def test_x3_matches_fp32_batch(x3_model):
     """B=3 random inputs (tile counts not a multiple of the grid) at three timesteps: the split
     mode against the fp32 mode of the same weights."""
@@ -128,7 +106,7 @@ def test_x3_matches_fp32_batch(x3_model):
     gt = torch.rand(3, 3, 256, 256, device=DEV, generator=g) * 2 - 1
     mask = (torch.rand(3, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
     t = torch.tensor([999, 500, 3], device=DEV)
-    m32 = DiffusionInpaintingModel(FULL, device=DEV)
+    m32 = DiffusionInpaintingModel(FULL, device=DEV, precision="fp32")
     m32.load_state_dict(make_state_dict(FULL, seed=1))
     with torch.no_grad():
         y3 = x3_model(x, t, masked_image=gt * (1 - mask), mask=mask)
@@ -153,7 +131,7 @@ def test_x3_matches_fp32_batch4(x3_model):
     gt = torch.rand(4, 3, 256, 256, device=DEV, generator=g) * 2 - 1
     mask = (torch.rand(4, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
     t = torch.tensor([999, 640, 120, 7], device=DEV)
-    m32 = DiffusionInpaintingModel(FULL, device=DEV)
+    m32 = DiffusionInpaintingModel(FULL, device=DEV, precision="fp32")
     m32.load_state_dict(make_state_dict(FULL, seed=1))
     with torch.no_grad():
         y3, ks = _kernels_run(x3_model, lambda: x3_model(x, t, masked_image=gt * (1 - mask), mask=mask))
@@ -176,7 +154,7 @@ def test_x3_matches_fp32_bench_batch(x3_model):
     gt = torch.rand(16, 3, 256, 256, device=DEV, generator=g) * 2 - 1
     mask = (torch.rand(16, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
     t = torch.tensor([999] * 8 + [250] * 8, device=DEV)
-    m32 = DiffusionInpaintingModel(FULL, device=DEV)
+    m32 = DiffusionInpaintingModel(FULL, device=DEV, precision="fp32")
     m32.load_state_dict(make_state_dict(FULL, seed=1))
     with torch.no_grad():
         y3 = x3_model(x, t, masked_image=gt * (1 - mask), mask=mask)
@@ -222,7 +200,7 @@ def test_x3_range_guard_forward(evals, record):
     sd = _scaled_state_dict()
     m3 = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16")
     m3.load_state_dict(sd)
-    m32 = DiffusionInpaintingModel(FULL, device=DEV)
+    m32 = DiffusionInpaintingModel(FULL, device=DEV, precision="fp32")
     m32.load_state_dict(sd)
     x, gt, mask = (_t(evals[f"full/{k}"]).to(DEV) for k in ("x", "gt", "mask"))
     t = torch.tensor([500], device=DEV)
