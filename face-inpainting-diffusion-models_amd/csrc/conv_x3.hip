@@ -173,9 +173,6 @@ __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int
   return t;
 }
 
-#ifndef X3_PREF
-#define X3_PREF 2
-#endif
 #ifndef X3_PINF
 #define X3_PINF 1
 #endif
@@ -397,9 +394,16 @@ __device__ __forceinline__ f32x16 xmfma(f16x8 a, f16x8 b, f32x16 c) {
 // MFMAs over one staged 3x3 chunk: 9 taps x (3 split products x 2 x 2 fragment blocks);
 // operand = the halo stage (planes of Geo::NP pixels, pb = halo pixel).
 // NPROD = 1 (the f16 precision mode): the hi x hi product only.
-template <int TW, int NPROD>
+struct NoSide {
+  template <int K>
+  __device__ __forceinline__ void step() const {}
+};
+
+// side.step<k>() runs after MFMA group k (k = 3 tap + group, 27 per chunk): work interleaved into the
+// MFMA stream (the residual prefetch of a unit's last chunks)
+template <int TW, int NPROD, class Side = NoSide>
 __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], f32x16 (&accl)[2][2], const lds_f* As, const lds_f* Ws,
-                                           const int (&pb)[2]) {
+                                           const int (&pb)[2], const Side& side = Side()) {
   using Geo = XGeo<TW>;
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const lds_f* Ah = As + 4 * (h * Geo::NP);
@@ -430,9 +434,9 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], f32x16 (&accl)[2
     fetch_bl(0);
     fetch_al(0);
   }
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    const int cur = tap & 1;
+  auto tap_step = [&](auto tapc) __attribute__((always_inline)) {
+    constexpr int tap = decltype(tapc)::value;
+    constexpr int cur = tap & 1;
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
@@ -440,8 +444,14 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], f32x16 (&accl)[2
         acc[mr][nr] = xmfma(ah[cur][mr], bs[cur][nr], acc[mr][nr]);
     __builtin_amdgcn_sched_barrier(0);
     if (tap + 1 < 9) fetch_hi(tap + 1, cur ^ 1);
+    side.template step<3 * tap>();
+    if (NPROD == 1) {  // one group per tap: all of the tap's side work here
+      side.template step<3 * tap + 1>();
+      side.template step<3 * tap + 2>();
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     __builtin_amdgcn_sched_barrier(0);
-    if (NPROD == 1) continue;
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
@@ -449,6 +459,7 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], f32x16 (&accl)[2
         accl[mr][nr] = xmfma(ah[cur][mr], bl[nr], accl[mr][nr]);
     __builtin_amdgcn_sched_barrier(0);
     if (tap + 1 < 9) fetch_bl(tap + 1);
+    side.template step<3 * tap + 1>();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int mr = 0; mr < 2; ++mr)
@@ -457,9 +468,49 @@ __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], f32x16 (&accl)[2
         accl[mr][nr] = xmfma(al[mr], bs[cur][nr], accl[mr][nr]);
     __builtin_amdgcn_sched_barrier(0);
     if (tap + 1 < 9) fetch_al(tap + 1);
+    side.template step<3 * tap + 2>();
     __builtin_amdgcn_sched_barrier(0);
-  }
+  };
+  tap_step(std::integral_constant<int, 0>{});
+  tap_step(std::integral_constant<int, 1>{});
+  tap_step(std::integral_constant<int, 2>{});
+  tap_step(std::integral_constant<int, 3>{});
+  tap_step(std::integral_constant<int, 4>{});
+  tap_step(std::integral_constant<int, 5>{});
+  tap_step(std::integral_constant<int, 6>{});
+  tap_step(std::integral_constant<int, 7>{});
+  tap_step(std::integral_constant<int, 8>{});
 }
+
+// The residual prefetch of a unit (identity or nearest-up residual) as side work of the MFMA stream:
+// the 64 loads of a lane's tile (register (mr, nr, r) = channel 32 nr + l32 of tile pixel
+// wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3)) go out 2-3 per MFMA group over one chunk instead of as one
+// 64-load burst ahead of it. Offsets: a per-mr lane base (nr * 128 as the immediate) + a wave-uniform
+// scalar part; the kind (identity / nearest-up) is a select, not a branch in the MFMA stream.
+template <int TW, int I0, int I1, int KN>  // loads [I0, I1) spread over MFMA groups 0 .. KN-1
+struct ResSide {
+  float (&rv)[2][2][16];
+  rsrc_t rr;
+  int vb[2];           // lane base per mr
+  int up;              // nearest-up residual
+  int W4, cout4;       // XF_NONE: output row width x cout x 4 B, cout x 4 B
+  int wm0, y0, x0, res_W;
+  template <int K>
+  __device__ __forceinline__ void step() const {
+    constexpr int lo = K < KN ? I0 + K * (I1 - I0) / KN : I1, hi = K < KN ? I0 + (K + 1) * (I1 - I0) / KN : I1;
+#pragma unroll
+    for (int i = lo; i < hi; ++i) {
+      const int mr = i >> 5, nr = (i >> 4) & 1, r = i & 15;
+      const int lin = 8 * (r >> 2) + (r & 3);
+      const int s_none = ((lin / TW) * W4) + (lin % TW) * cout4;
+      const int ub = wm0 + 32 * mr + 8 * (r >> 2);
+      const int yy = (y0 + ub / TW) >> 1, xx = ((x0 + ub % TW) >> 1) + ((r & 3) >> 1);
+      const int s_up = (yy * res_W + xx) * cout4;
+      rv[mr][nr][r] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb[mr] + nr * 128, up ? s_up : s_none, 0));
+    }
+  }
+};
 
 template <int XF, bool SKIP, int TW, int NPROD>
 __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
@@ -534,39 +585,9 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     };
     // SKIP kernels have no residual (the host runs a 1x1 conv with a residual, proj_out, split-K: the
     // reduction adds it). Its 64 registers would not fit beside the skip operand buffers.
-    auto prefetch = [&](const STile& t, float (&rv)[2][2][16]) {
+    auto bias_load = [&](const STile& t) {
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr) bias2[nr] = gld1(p.bias + t.ct * XBN + 32 * nr + l32);
-      if (SKIP || !p.res) return;
-      const rsrc_t rr = mkrsrc(p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout);
-      if (p.res_xform == XF_NONE) {
-        const int vb = vbase(t);
-#pragma unroll
-        for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-          for (int nr = 0; nr < 2; ++nr)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              rv[mr][nr][r] = __builtin_bit_cast(
-                  float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb + mr * mstep + nr * 128, roff(r), 0));
-      } else {  // XF_UP: nearest-upsampled residual (XF_DOWN residuals arrive pre-pooled)
-        // tile pixel wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3): the first three terms are wave-uniform and a
-        // multiple of 8 (TW >= 8), so the source pixel's row is uniform and its column is a uniform part
-        // + 2 h + ((r & 3) >> 1): one lane base, the rest scalar offsets (per-register VGPR addresses
-        // spilled once the correction accumulators took their registers)
-        const int vb = (2 * h * p.cout + t.ct * XBN + l32) * 4;
-#pragma unroll
-        for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ub = wm0 + 32 * mr + 8 * (r >> 2);
-            const int y = (t.y0 + ub / TW) >> 1, x = ((t.x0 + ub % TW) >> 1) + ((r & 3) >> 1);
-            const int so = (y * p.res_W + x) * p.cout * 4;
-#pragma unroll
-            for (int nr = 0; nr < 2; ++nr)
-              rv[mr][nr][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb + nr * 128, so, 0));
-          }
-      }
     };
     auto epilogue = [&](const STile& t, int z, const float (&rv)[2][2][16], bool tstamp = false) {
       if (X3_ABLATE == 13) {  // timing only: no epilogue
@@ -793,6 +814,18 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         ++j;
         XBARRIER_CONSUMER();
       };
+      auto main_chunk_side = [&](bool sep, const auto& side) __attribute__((always_inline)) {
+        stamp(j);
+        if (X3_ABLATE != 4) {
+          if (sep)
+            consume_x3<TW, NPROD>(acc, accl, A0 + (j & 1) * XA, W0 + (j % 3) * XW, pb, side);
+          else
+            consume_x3<TW, NPROD>(acc, acc, A0 + (j & 1) * XA, W0 + (j % 3) * XW, pb, side);
+        }
+        stamp(j, 16);
+        ++j;
+        XBARRIER_CONSUMER();
+      };
       // the correction sum joins the main one (one rounding per output) before the unit's last 3x3
       // chunk: from there on accl is dead and its registers hold the residual / skip-operand prefetch
       auto fold = [&]() __attribute__((always_inline)) {
@@ -810,13 +843,50 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       // not a loop-carried value. The two cases are separate branches so that the operand buffers are
       // defined on every path to their use (otherwise they would stay live across all 3x3 chunks).
       if (!has_skip) {
-        // the residual / bias prefetch goes out X3_PREF chunks before the unit's end (peeled)
-        constexpr int PF = X3_PREF;
-        for (int c = c0; c < me - PF; ++c) main_chunk(true);
+        // The residual (64 loads per lane) goes out during the unit's last two 3x3 chunks, interleaved
+        // into their MFMA groups: the mr = 0 half spread over the whole of chunk me - 2 (which still
+        // accumulates the corrections in accl), then the fold, then the mr = 1 half over the first third
+        // of chunk me - 1 (its correction products go to acc). Peak: acc + accl + fragments + half the
+        // residual, or acc + fragments + the residual.
+        const bool rpf = !SKIP && S == 1 && p.res;
+        for (int c = c0; c < me - 2; ++c) main_chunk(true);
         if (me > c0) {
-          fold();
-          if (!SKIP && S == 1) prefetch(t, rv);
-          for (int c = (me - PF > c0 ? me - PF : c0); c < me; ++c) main_chunk(false);
+          // the lane's id re-read here (volatile: not hoisted, so no per-lane address lives through the
+          // whole unit loop for these loads: such values were spilled, and the reload's vmcnt(0) waited
+          // on the loads in flight)
+          int ln;
+          asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+          const int lh = ln >> 5, ll = ln & 31;
+          if (!SKIP && S == 1) {
+            const rsrc_t rb = mkrsrc(p.bias);
+#pragma unroll
+            for (int nr = 0; nr < 2; ++nr)
+              bias2[nr] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, 4 * ll, 4 * (t.ct * XBN + 32 * nr), 0));
+          }
+          const int up = p.res_xform != XF_NONE;
+          const int cu = t.ct * XBN;
+          const int vn = (((wimg * p.H + t.y0 + wrow) * p.W + t.x0 + 4 * lh) * p.cout + cu + ll) * 4;
+          const int vu = (2 * lh * p.cout + cu + ll) * 4;
+          const rsrc_t rr = mkrsrc(p.res ? p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout : p.bias);
+          const int vb0 = up ? vu : vn, vb1 = up ? vu : vn + mstep;
+          const int W4 = p.W * p.cout * 4, c4 = p.cout * 4;
+          if (me - c0 >= 2) {
+            if (rpf)
+              main_chunk_side(true, ResSide<TW, 0, 32, 27>{rv, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+            else
+              main_chunk(true);
+            fold();
+            if (rpf)
+              main_chunk_side(false, ResSide<TW, 32, 64, 9>{rv, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+            else
+              main_chunk(false);
+          } else {  // a one-chunk unit: all of the residual in its first third
+            fold();
+            if (rpf)
+              main_chunk_side(false, ResSide<TW, 0, 64, 9>{rv, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+            else
+              main_chunk(false);
+          }
         }
       } else {
         skip_setup(t);
@@ -850,7 +920,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           if (sk + 1 < se) skip_step(sq1, false, 0);
         }
       }
-      if (SKIP && S == 1) prefetch(t, rv);  // (bias only: SKIP kernels have no residual)
+      if (SKIP && S == 1) bias_load(t);  // (SKIP kernels have no residual)
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
         p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
       epilogue(t, z, rv, u == 0);

@@ -217,7 +217,9 @@ def test_train_x3_head_dgrad_fallback(record):
         torch.cuda.synchronize()
         assert tr.guard_trips == 0
         if decline:
-            assert declined == [16]  # the padded operand was offered, declined, and the fp32 path ran
+            # the padded operand was offered and declined; conv() then offers the unpadded 8-channel
+            # gradient (declined too) and runs the fp32 kernel on it
+            assert declined == [16, 8]
         res[prec] = (loss, tr.grad.clone(), tr.offsets)
         del tr
     (l32, g32, offs), (l3, g3, _) = res["fp32"], res["3xf16"]
