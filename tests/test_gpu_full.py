@@ -6,16 +6,18 @@ importing the reference). Every measured error is recorded (conftest `record`).
 Tolerances (written here, fp32 class throughout):
   * C2 / C3 full loops vs the reference:           max-abs < 1e-4 (north_star), both modes
   * UNet eval error vs an fp64 UNet (C1's eval):   3xf16 (the default mode): mean and p99.9 within
-                                                   2x of the fp32 reference's own error vs fp64,
-                                                   max within 4x. fp32 mode: 3x / 4x — its MFMA
-                                                   chain sums K = 9 Cin terms sequentially in one
-                                                   accumulator (measured 2.6x oneDNN's mean error;
-                                                   the f16 MFMA sums 16 products per rounding)
-  * C1 10-step loops vs the fp64 loop:             both modes: the rel-1e-5 perturbation envelope of
-                                                   golden/conditioning.json (max, p99.9) - the spread of
-                                                   an fp32 UNet whose rounding differs from oneDNN's;
-                                                   the 3xf16 loop measures past the rel-1e-6 envelope
-                                                   (DESIGN.md §4 records the cause)
+                                                   1.5x of the fp32 reference's own error vs fp64,
+                                                   max within 2x (measured 1.16x / 1.15x / 1.21x).
+                                                   fp32 mode: 3x / 4x — its MFMA chain sums K = 9 Cin
+                                                   terms sequentially in one accumulator with one
+                                                   rounding per product (measured 2.6x oneDNN's mean)
+  * C1 10-step loops vs the fp64 loop:             3xf16: p99.9 within 2x of the reference's own
+                                                   p99.9 vs the fp64 loop, max within 2.5x (measured
+                                                   1.40x / 2.08x at eta 0). The max is a tail statistic
+                                                   of a chaotic loop: a rel-1e-6 perturbation of eps
+                                                   alone moves it by 4.4e-3 = 4.9x the reference's
+                                                   (golden/conditioning.json). fp32 mode: the rel-1e-5
+                                                   perturbation envelope (max, p99.9)
   * advanced-inpainting loops vs the fp64 loop:    max-abs within max(1e-4, 4x the reference's)
   * sharded vs unsharded (batch_invariant option): bit-identical
 """
@@ -124,7 +126,7 @@ def _ddpm_steps(model, gt, mask, steps, seed, noise_shard=None):
 
 @pytest.mark.parametrize("prec", PRECISIONS)
 def test_c3_batch64_ddpm_steps(record, prec):
-    """The C3 workload size (B=64 at 256x256, ~13 GB of workspace): three fused DDPM steps are
+    """The C3 workload size (B=64 at 256x256, 17.4 GB of workspace): three fused DDPM steps are
     finite, and with the batch-invariant geometry images 0, 37 and 63 equal their own B=1 runs
     (noise drawn for the full batch and sliced) bit for bit."""
     from bench import synth_inputs
@@ -173,9 +175,9 @@ def test_c1_eval_error_vs_fp64(meta_full, record, prec):
     s_gpu = _stats(y, _t(g["y64"]))
     s_ref = meta_full["envelopes"]["c1_eval0"]
     record(f"c1_eval0/{prec}", gpu_vs_fp64=s_gpu, reference_vs_fp64=s_ref, gpu_vs_reference=_stats(y, _t(g["y32"])))
-    k = 2 if prec == "3xf16" else 3
+    k, km = (1.5, 2) if prec == "3xf16" else (3, 4)
     assert s_gpu["mean"] <= k * s_ref["mean"] and s_gpu["p999"] <= k * s_ref["p999"]
-    assert s_gpu["max"] <= 4 * s_ref["max"]
+    assert s_gpu["max"] <= km * s_ref["max"]
 
 
 @pytest.mark.parametrize("prec", PRECISIONS)
@@ -186,11 +188,10 @@ def test_c1_loop_vs_fp64(meta, meta_full, loops, record, prec, name):
     fp64 oracle loop (exact arithmetic, same noise), next to the fp32 reference's own error.
     The loop is chaotic at the rounding level: two builds of the split kernels whose outputs along
     the same trajectory differ by 1e-7 (mean) and sit equally far from fp32 at every step
-    (tools/diag/c1_states.py) end 1e-3 and 9e-3 (max) from fp64. So the accuracy claim is carried
-    by the per-eval gate (test_c1_eval_error_vs_fp64: mean and p99.9 within 2x of the reference's own
-    fp64 error in 3xf16) and
-    this gate is the rel-1e-5 perturbation envelope of tests/golden/conditioning.json (max, p99.9)
-    for both modes: the spread any fp32 UNet whose rounding differs from oneDNN's must expect."""
+    (tools/diag/c1_states.py) ended 1e-3 and 9e-3 (max) from fp64. 3xf16 (the default): p99.9 within
+    2x and max within 2.5x of the reference's own error against the same fp64 loop. fp32 mode (one
+    rounding per product over K = 9 Cin, 2.6x the reference's per-eval error): the rel-1e-5
+    perturbation envelope of tests/golden/conditioning.json (max, p99.9)."""
     import json
     import os
     cond = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "conditioning.json")))
@@ -204,8 +205,12 @@ def test_c1_loop_vs_fp64(meta, meta_full, loops, record, prec, name):
     record(f"{name}/{prec}", gpu_vs_fp64=s64, gpu_vs_reference=s_ref,
            reference_vs_fp64=meta_full["envelopes"][name],
            envelope={"max": max(v["max"] for v in env), "p999": max(v["p999"] for v in env)})
-    assert s64["max"] <= max(1e-3, max(v["max"] for v in env))
-    assert s64["p999"] <= max(1e-4, max(v["p999"] for v in env))
+    r = meta_full["envelopes"][name]
+    if prec == "3xf16":
+        assert s64["p999"] <= 2 * r["p999"] and s64["max"] <= 2.5 * r["max"], (s64, r)
+    else:
+        assert s64["max"] <= max(1e-3, max(v["max"] for v in env))
+        assert s64["p999"] <= max(1e-4, max(v["p999"] for v in env))
 
 
 @pytest.mark.parametrize("prec", PRECISIONS)
