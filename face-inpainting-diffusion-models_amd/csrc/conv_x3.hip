@@ -396,14 +396,14 @@ __device__ __forceinline__ f32x16 xmfma(f16x8 a, f16x8 b, f32x16 c) {
 // NPROD = 1 (the f16 precision mode): the hi x hi product only.
 struct NoSide {
   template <int K>
-  __device__ __forceinline__ void step() const {}
+  __device__ __forceinline__ void step() {}
 };
 
 // side.step<k>() runs after MFMA group k (k = 3 tap + group, 27 per chunk): work interleaved into the
 // MFMA stream (the residual prefetch of a unit's last chunks)
 template <int TW, int NPROD, class Side = NoSide>
 __device__ __forceinline__ void consume_x3(f32x16 (&acc)[2][2], f32x16 (&accl)[2][2], const lds_f* As, const lds_f* Ws,
-                                           const int (&pb)[2], const Side& side = Side()) {
+                                           const int (&pb)[2], Side&& side = Side()) {
   using Geo = XGeo<TW>;
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const lds_f* Ah = As + 4 * (h * Geo::NP);
@@ -550,25 +550,29 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       const int mi = m / (Geo::TH * TW), mp = m % (Geo::TH * TW);  // image of the tile, its pixel
       pb[mr] = mi * Geo::HP + (mp / TW) * Geo::HW + (mp % TW);
     }
+    // acc at the unit's start; accl just before its first use (after a deferred-epilogue chunk, whose
+    // final values need the registers)
     auto zero = [&]() {
 #pragma unroll
       for (int mr = 0; mr < 2; ++mr)
 #pragma unroll
         for (int nr = 0; nr < 2; ++nr)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            acc[mr][nr][r] = 0.f;
-            accl[mr][nr][r] = 0.f;
-          }
+          for (int r = 0; r < 16; ++r) acc[mr][nr][r] = 0.f;
+    };
+    auto zero_l = [&]() {
+#pragma unroll
+      for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) accl[mr][nr][r] = 0.f;
     };
     // Epilogue straight from the accumulators. Lane (h, l32) holds channel 32 nr + l32 of tile
     // pixel wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3) (column offset 4 h + (r & 3) < 8 stays in
     // its row): one dword store per register = two 128-B row segments. Bias and residual are
     // loaded in the same layout while the unit's last chunk is on the MFMAs, so the epilogue
     // waits on nothing and its stores drain behind the next unit's chunks.
-    // rv (the residual prefetch) is declared per unit, inside the unit loop: declared out here, a unit
-    // without a prefetch (split-K, no residual) would carry the previous unit's values, so the 64
-    // registers would be live through every chunk
     float bias2[2];
     // Register (mr, r) of lane (h, l32) sits at tile pixel wm0 + 32 mr + 8 (r >> 2) + 4 h + (r & 3).
     // Byte offsets: vbase (lane: tile origin, the wave's rows, 4 h, channel) + mr * mstep (lane) +
@@ -580,8 +584,17 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     const int mstep = (32 / TW) * p.W * p.cout * 4;
     // the wave's 64 pixels: rows of one image (8x8 tiles: the whole image wm0 / 64 of the tile)
     const int wimg = wm0 / (Geo::TH * TW), wrow = (wm0 % (Geo::TH * TW)) / TW;
+    // the lane id re-read where a lane-dependent address is needed once per unit (volatile: not hoisted),
+    // so that no such address lives through the chunk loop (they were spilled, and the reloads' vmcnt(0)
+    // waited for the loads or stores in flight)
+    auto lane_id = [&]() {
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      return ln;
+    };
     auto vbase = [&](const STile& t) {
-      return (((wimg * p.H + t.y0 + wrow) * p.W + t.x0 + 4 * h) * p.cout + t.ct * XBN + l32) * 4;
+      const int ln = lane_id();
+      return (((wimg * p.H + t.y0 + wrow) * p.W + t.x0 + 4 * (ln >> 5)) * p.cout + t.ct * XBN + (ln & 31)) * 4;
     };
     // SKIP kernels have no residual (the host runs a 1x1 conv with a residual, proj_out, split-K: the
     // reduction adds it). Its 64 registers would not fit beside the skip operand buffers.
@@ -676,14 +689,18 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           merge(IFD_QP(mean[nr], 0x44), IFD_QP(m2[nr], 0x44), IFD_QP(mean[nr], 0xEE), IFD_QP(m2[nr], 0xEE), 128.f, mean[nr],
                 m2[nr]);
 #undef IFD_QP
-        if (h == 0 && (l32 & 3) == 0) {
+        // through a buffer descriptor (scalar base, lane offset from a fresh lane id): a 64-bit per-lane
+        // pointer here was spilled, and its reload's vmcnt(0) waited for the unit's 64 output stores
+        const int ln = lane_id();
+        if (ln < 32 && (ln & 3) == 0) {
           const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
+          const rsrc_t rg = mkrsrc(p.gstat + (size_t)(t.n0 + wimg) * (p.cout / 4) * p.gstat_E * 2);
+          const int vo = (ln >> 2) * p.gstat_E * 8;
 #pragma unroll
           for (int nr = 0; nr < 2; ++nr) {
-            float* o = p.gstat + (((size_t)(t.n0 + wimg) * (p.cout / 4) + t.ct * 16 + nr * 8 + (l32 >> 2)) *
-                                      p.gstat_E + e) * 2;
-            o[0] = mean[nr];
-            o[1] = m2[nr];
+            const int so = ((t.ct * 16 + nr * 8) * p.gstat_E + e) * 8;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mean[nr]), rg, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m2[nr]), rg, vo + 4, so, 0);
           }
         }
       }
@@ -791,10 +808,12 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
     if (IFD_TRACE && p.trace && wave == 0 && lane == 0) p.trace[64 * blockIdx.x + 58] = __builtin_amdgcn_s_memtime();
     XBARRIER_CONSUMER();  // chunk 0 staged
     int j = 0;  // position in the block's chunk stream: ring slot j % 3, A stage j & 1
+    // xr: the residual prefetch of a unit's last two chunks (declared out here with the epilogue's values
+    // in the same registers; a per-unit declaration gave the allocator two homes and copies between them)
+    float xr[2][2][16];
     for (int u = 0; u < nu; ++u) {
       int z;
       const STile t = unit_of(u, z);
-      float rv[2][2][16];
       zero();  // (here, not after the epilogue: the zeros of the next unit are then not live through this one)
       // the unit's K range [c0, c1): 3x3 chunks [c0, me), then skip chunks [sb, se) of the 1x1 segment
       const int c0 = z * nchu, c1 = c0 + nchu;
@@ -814,7 +833,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         ++j;
         XBARRIER_CONSUMER();
       };
-      auto main_chunk_side = [&](bool sep, const auto& side) __attribute__((always_inline)) {
+      auto main_chunk_side = [&](bool sep, auto&& side) __attribute__((always_inline)) {
         stamp(j);
         if (X3_ABLATE != 4) {
           if (sep)
@@ -849,13 +868,13 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         // of chunk me - 1 (its correction products go to acc). Peak: acc + accl + fragments + half the
         // residual, or acc + fragments + the residual.
         const bool rpf = !SKIP && S == 1 && p.res;
+        zero_l();
         for (int c = c0; c < me - 2; ++c) main_chunk(true);
         if (me > c0) {
           // the lane's id re-read here (volatile: not hoisted, so no per-lane address lives through the
           // whole unit loop for these loads: such values were spilled, and the reload's vmcnt(0) waited
           // on the loads in flight)
-          int ln;
-          asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+          const int ln = lane_id();
           const int lh = ln >> 5, ll = ln & 31;
           if (!SKIP && S == 1) {
             const rsrc_t rb = mkrsrc(p.bias);
@@ -872,24 +891,25 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           const int W4 = p.W * p.cout * 4, c4 = p.cout * 4;
           if (me - c0 >= 2) {
             if (rpf)
-              main_chunk_side(true, ResSide<TW, 0, 32, 27>{rv, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+              main_chunk_side(true, ResSide<TW, 0, 32, 27>{xr, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
             else
               main_chunk(true);
             fold();
             if (rpf)
-              main_chunk_side(false, ResSide<TW, 32, 64, 9>{rv, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+              main_chunk_side(false, ResSide<TW, 32, 64, 9>{xr, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
             else
               main_chunk(false);
           } else {  // a one-chunk unit: all of the residual in its first third
             fold();
             if (rpf)
-              main_chunk_side(false, ResSide<TW, 0, 64, 9>{rv, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+              main_chunk_side(false, ResSide<TW, 0, 64, 9>{xr, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
             else
               main_chunk(false);
           }
         }
       } else {
         skip_setup(t);
+        zero_l();
         for (int c = c0; c < me - 1; ++c) main_chunk(true);
         fold();
         // one definition point per operand buffer on every path (a buffer defined in two branches
@@ -923,7 +943,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       if (SKIP && S == 1) bias_load(t);  // (SKIP kernels have no residual)
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
         p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
-      epilogue(t, z, rv, u == 0);
+      epilogue(t, z, xr, u == 0);
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0) {
         __builtin_amdgcn_s_waitcnt(0);  // (trace builds: wait for the stores to leave)
         p.trace[64 * blockIdx.x + 63] = __builtin_amdgcn_s_memtime();    // first epilogue: end
