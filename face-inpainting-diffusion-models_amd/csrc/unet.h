@@ -87,8 +87,8 @@ class Model {
   int set_precision(int prec);
   int precision() const { return prec_; }
   // Handle options (ifd_set_option): initial values come from the environment once, at creation
-  // (IFD_CONV_STREAM, IFD_X3_OFF, IFD_GN_FUSED, IFD_STREAM_CW, IFD_CONV_BM, IFD_CONV_LDS_PAD,
-  // IFD_BATCH_INVARIANT); nothing is read from the environment per launch.
+  // (IFD_CONV_STREAM, IFD_X3_OFF, IFD_GN_FUSED, IFD_SKIP_SEP, IFD_BATCH_INVARIANT); nothing is read from
+  // the environment per launch.
   int set_option(const std::string& key, int value);
   int get_option(const std::string& key, int* value) const;
 

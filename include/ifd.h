@@ -96,14 +96,15 @@ int ifd_get_precision(ifd_handle* h, int* prec);
 /* Handle options. No reference counterpart: execution choices of this library that never change
  * the arithmetic of a single image except where noted. Initial values are read from the
  * environment once, in ifd_create (IFD_BATCH_INVARIANT, IFD_CONV_STREAM, IFD_GN_FUSED, IFD_X3_OFF,
- * IFD_STREAM_CW, IFD_CONV_BM=128, IFD_CONV_LDS_PAD); nothing is read per launch. Keys:
+ * IFD_SKIP_SEP); nothing is read per launch. Keys:
  *   "batch_invariant" 0/1  tile kind and split-K chosen per image, so an image's output is
  *                          bit-identical whatever batch it shares a launch with (multi-GPU parity
  *                          mode: N ranks x B/N images == one rank x B images). Slower on small layers.
  *   "conv_stream"     0..2 wide fp32 layers: one tile per workgroup / persistent 1 or 2 per CU
  *   "gn_fused"        0/1  GroupNorm statistics fused into the producing conv (1) or a separate pass
- *   "x3_off", "stream_cw", "conv_bm128", "lds_pad"   development switches (bisecting, tuning; x3_off
- *                          bit 32 keeps the output head on the fp32 VALU kernel in the 3xf16 mode) */
+ *   "skip_sep"        >= 0 split modes: a ResBlock's 1x1 skip as its own launch at resolutions >= this
+ *   "x3_off"               bisecting mask of the split kernels (bit 32 keeps the output head on the
+ *                          fp32 VALU kernel in the 3xf16 mode) */
 int ifd_set_option(ifd_handle* h, const char* key, int value);
 int ifd_get_option(ifd_handle* h, const char* key, int* value);
 /* Bytes of device workspace the handle holds (weights + activations). */
