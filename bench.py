@@ -189,7 +189,7 @@ def train_main(args):
     torch.cuda.set_device(dev)
     parallel.init(device=dev)
     B, H = args.batch, FULL.image_size
-    prec = "fp32" if args.precision == "fp32" else "3xf16"
+    prec = args.precision
     diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="quadratic")
     gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
     masked = gt * (1 - mask)
@@ -227,7 +227,8 @@ def train_main(args):
            "unit": "images/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None,
-           "dtype": "f32" if prec == "fp32" else "f32 (3xf16 split MFMA for the forward, dgrad and wgrad 3x3 convs)",
+           "dtype": {"fp32": "f32", "3xf16": "f32 (3xf16 split MFMA for the forward, dgrad and wgrad 3x3 convs)",
+                     "f16": "f16 operands, fp32 accumulate (reduced precision, not fp32-class)"}[prec],
            "data": "synthetic (gt~U(-1,1), rectangle masks, seeded weights)",
            "config": {"workload": "train_inpainting.py train_epoch step (BASELINE configs[4]; the reference trains "
                                   "fp32 and has no bf16/LoRA)", "global_batch": B * ws, "batch_per_gpu": B,
@@ -239,6 +240,13 @@ def train_main(args):
         res["fp32_exact"] = {"value": round(B * args.fp32_exact_steps / el2, 4), "unit": "images/s",
                              "ms_per_step": round(el2 / args.fp32_exact_steps * 1e3, 2),
                              "steps": args.fp32_exact_steps}
+    if ws == 1 and args.f16_steps > 0 and prec == "3xf16":
+        # the reduced-precision variant (BASELINE configs[4]'s "bf16" wording; not fp32-class), timed separately
+        el3, l3, t3 = run("f16", args.f16_steps, 1)
+        res["f16_reduced"] = {"value": round(B * args.f16_steps / el3, 4), "unit": "images/s",
+                              "ms_per_step": round(el3 / args.f16_steps * 1e3, 2), "steps": args.f16_steps,
+                              "loss": l3, "guard_trips": t3,
+                              "dtype": "f16 operands, fp32 accumulate (tests/test_gpu_train.py::test_train_f16_full_vs_fp32)"}
     if rank == 0:
         print(json.dumps(res), flush=True)
 

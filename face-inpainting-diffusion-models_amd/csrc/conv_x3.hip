@@ -119,38 +119,31 @@ struct XGeo {
 constexpr int XDMA3 = 9, XDMA1 = XWS / 4 / NP_T;
 
 // Work unit L -> (tile, split z). The S splits of a tile are consecutive L; pixel tiles in groups
-// of 8 get channel-tile IDs 8 apart (conv.hip's XCD-aware map) when the tile count allows. Every
+// of 8 get channel-tile IDs 8 apart (conv.hip's XCD-aware map) when the tile count allows: block b
+// runs units L = b + u G, and blocks b and b + 8 sit on the same XCD (workgroups are dealt to the 8
+// XCDs round robin), so the channel tiles of a pixel tile run at the same time on one XCD and fetch
+// their shared input (halo, skip operand) from HBM once. (Round 3's alternative, a block running the
+// channel tiles of one pixel tile back to back, measured 1 % slower per eval: profiles/r04a.) Every
 // divisor is a power of two (run_conv requires power-of-two sizes; S, cout / 64 in {1, 2, 4, 8}),
 // so the decode is shifts and masks on log2 values taken once per kernel.
 struct XDec {
   int lks, lnct, ltx, lty, limg;
-  bool xcd;        // conv.hip's XCD-aware map (pixel tiles in groups of 8)
-  bool blk_major;  // a block's consecutive units = the channel tiles of one pixel tile
-  int nct;         // channel tiles; not a power of two (the 1536-wide qkv 1x1): decoded by division
+  bool xcd;  // conv.hip's XCD-aware map (pixel tiles in groups of 8)
+  int nct;   // channel tiles; not a power of two (the 1536-wide qkv 1x1): decoded by division
   bool pow2;
 };
 __device__ __forceinline__ XDec x3_dec(const ConvParams& p, int nct) {
   const bool pow2 = (nct & (nct - 1)) == 0;
   return {__builtin_ctz(p.ksplit), __builtin_ctz(nct), __builtin_ctz(p.tiles_x), __builtin_ctz(p.tiles_y),
-          __builtin_ctz(p.IMGS), pow2 && p.npix_tiles % 8 == 0,
-          p.ksplit == 1 && p.npix_tiles % (int)gridDim.x == 0, nct, pow2};
+          __builtin_ctz(p.IMGS), pow2 && p.npix_tiles % 8 == 0, nct, pow2};
 }
-// Unit u of block b. blk_major (no split-K, pixel tiles a multiple of the grid): block b takes
-// pixel tiles b, b + G, ... and runs all channel tiles of each back to back, so the second
-// channel tile re-reads the same input (3x3 halo and skip operand) from L2 instead of HBM.
-// Otherwise L = b + u G walks the XCD-aware map (S splits of a tile consecutive in L).
-// NP2: non-power-of-two channel-tile counts allowed (the 1x1-only launches, which use the SKIP
-// instantiations; the others keep the shift-only decode and its register budget)
+// Unit u of block b. NP2: non-power-of-two channel-tile counts allowed (the 1x1-only launches, which
+// use the SKIP instantiations; the others keep the shift-only decode and its register budget)
 template <bool NP2>
 __device__ __forceinline__ STile x3_unit(const ConvParams& p, const XDec& d, int b, int u, int& z) {
   STile t;
   int bx;
-  if (d.blk_major) {
-    z = 0;
-    const int uq = (!NP2 || d.pow2) ? u >> d.lnct : u / d.nct;
-    t.ct = u - uq * d.nct;
-    bx = b + (int)gridDim.x * uq;
-  } else {
+  {
     const int L = b + u * (int)gridDim.x;
     z = L & ((1 << d.lks) - 1);
     const int v = L >> d.lks;

@@ -392,7 +392,9 @@ struct WxCfg {
 // split's pixels per channel (fixed order: per thread over chunks, then the pixel lanes in lane
 // order) into colpart[split][cout]; colsum_final_kernel adds the splits in order.
 // TAPS = 9 (3x3, halo of one pixel) or 1 (1x1: the chunk's own pixels, no halo).
-template <int TAPS>
+// NPROD = 3 (fp32-class: three split products) or 1 (the reduced-precision f16 training mode: the hi x hi
+// product only; no lo planes are staged or read).
+template <int TAPS, int NPROD>
 __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
   using Cf = WxCfg<TAPS>;
   constexpr int NT = Cf::NT, WX_DI = Cf::DI, WX_XI = Cf::XI, NTMAX = Cf::NTMAX;
@@ -506,10 +508,10 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
         const int o = wx_off(row, 4 * cq);
         if (isd) {
           *(wx_lds_u2*)(L + o) = hi;
-          *(wx_lds_u2*)(L + WX_PX * WX_P + o) = lo;
+          if (NPROD == 3) *(wx_lds_u2*)(L + WX_PX * WX_P + o) = lo;
         } else {
           *(wx_lds_u2*)(X + o) = hi;
-          *(wx_lds_u2*)(X + WX_HMAX * WX_P + o) = lo;
+          if (NPROD == 3) *(wx_lds_u2*)(X + WX_HMAX * WX_P + o) = lo;
         }
       }
     };
@@ -544,20 +546,28 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       const _Float16* pB = Xh + ((Wc >= 16 ? 8 * hl : hl * HWc) + ql) * WX_P + cBl;
       auto fetchA = [&](int st, wx_h8& ahi, wx_h8& alo) {
         const _Float16* b = pA + 16 * st * WX_P;
-        const wx_h4 ah0 = wx_tr(b, 0), ah1 = wx_tr(b, 4 * WX_P), al0 = wx_tr(b, WX_PX * WX_P),
-                    al1 = wx_tr(b, WX_PX * WX_P + 4 * WX_P);
+        const wx_h4 ah0 = wx_tr(b, 0), ah1 = wx_tr(b, 4 * WX_P);
         ahi = wx_h8{ah0[0], ah0[1], ah0[2], ah0[3], ah1[0], ah1[1], ah1[2], ah1[3]};
-        alo = wx_h8{al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
+        if (NPROD == 3) {
+          const wx_h4 al0 = wx_tr(b, WX_PX * WX_P), al1 = wx_tr(b, WX_PX * WX_P + 4 * WX_P);
+          alo = wx_h8{al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
+        } else {
+          alo = ahi;
+        }
       };
       auto fetchB = [&](int st, int t, wx_h8& bhi, wx_h8& blo) {
         const int m0 = 16 * st;  // (wave-uniform part of the k-step's first pixel)
         const int hb = Wc >= 16 ? (m0 >> lwc) * HWc + (m0 & (Wc - 1)) : 2 * st * HWc;
         const int r0 = TAPS == 9 ? hb + (t / 3) * HWc + (t % 3) : hb;
         const _Float16* b = pB + __builtin_amdgcn_readfirstlane(r0 * WX_P);
-        const wx_h4 bh0 = wx_tr(b, 0), bh1 = wx_tr(b, 4 * WX_P), bl0 = wx_tr(b, WX_HMAX * WX_P),
-                    bl1 = wx_tr(b, WX_HMAX * WX_P + 4 * WX_P);
+        const wx_h4 bh0 = wx_tr(b, 0), bh1 = wx_tr(b, 4 * WX_P);
         bhi = wx_h8{bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
-        blo = wx_h8{bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
+        if (NPROD == 3) {
+          const wx_h4 bl0 = wx_tr(b, WX_HMAX * WX_P), bl1 = wx_tr(b, WX_HMAX * WX_P + 4 * WX_P);
+          blo = wx_h8{bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
+        } else {
+          blo = bhi;
+        }
       };
       constexpr int NST = WX_PX / 16, NPAIR = (NTAP + 1) / 2;
       wx_h8 ahi, alo, b0h, b0l, b1h, b1l;
@@ -591,10 +601,12 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
           if (WX_IL && nxt && WX_ABL != 3)  // (block-uniform)
 #pragma unroll
             for (int q = pp; q < (pp + 1 == NPAIR ? WX_PER : pp + 1); ++q) store_item(Ln, st * WX_PER + q, SETc);
-          acc[l0] = WX_MFMA(ahi, b0l, acc[l0], 0, 0, 0);
-          if (two) acc[l1] = WX_MFMA(ahi, b1l, acc[l1], 0, 0, 0);
-          acc[l0] = WX_MFMA(alo, b0h, acc[l0], 0, 0, 0);
-          if (two) acc[l1] = WX_MFMA(alo, b1h, acc[l1], 0, 0, 0);
+          if (NPROD == 3) {
+            acc[l0] = WX_MFMA(ahi, b0l, acc[l0], 0, 0, 0);
+            if (two) acc[l1] = WX_MFMA(ahi, b1l, acc[l1], 0, 0, 0);
+            acc[l0] = WX_MFMA(alo, b0h, acc[l0], 0, 0, 0);
+            if (two) acc[l1] = WX_MFMA(alo, b1h, acc[l1], 0, 0, 0);
+          }
           __builtin_amdgcn_sched_barrier(0);
           if (more) {
             b0h = n0h; b0l = n0l;
@@ -1720,15 +1732,15 @@ int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int 
                    int cin_pad, int cout, const float* res, float* out, float* part, int64_t part_floats,
                    unsigned* guard, void* stream) {
   return ifd_tr_conv_x3_taps(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, 9,
-                             stream);
+                             3, stream);
 }
 
 static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
                        const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
                        int64_t part_floats, unsigned* guard, int wx3_taps, float* gstat, int64_t gstat_floats,
-                       int* gstat_E, float* gstat_cnt, void* stream) {
+                       int* gstat_E, float* gstat_cnt, int nprod, void* stream) {
   if (gstat_E) *gstat_E = 0;
-  if ((H & (H - 1)) || c0 + c1 != cin_pad || !x0 || !out || !wx3 || !bias || !guard) {
+  if ((H & (H - 1)) || c0 + c1 != cin_pad || !x0 || !out || !wx3 || !bias || !guard || (nprod != 1 && nprod != 3)) {
     set_error("ifd_tr_conv_x3: unsupported arguments");
     return 2;
   }
@@ -1740,6 +1752,7 @@ static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, 
   }
   conv_x3_params(p, x0, c0, c1 ? x1 : nullptr, c1, N, H, wx3, bias, cin_pad, cout, res, out, taps);
   p.guard = guard;
+  p.x3_nprod = nprod;
   const int nct = cout / 64;  // the non-SKIP split kernel decodes channel tiles by shifts
   if (cout % 64 || (taps == 9 && (nct & (nct - 1))) || !conv_x3_eligible(p, taps, XF_NONE, 64)) {
     set_error("ifd_tr_conv_x3: shape not eligible for the split kernel (use ifd_tr_conv)");
@@ -1788,9 +1801,9 @@ static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, 
 
 int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
                         const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
-                        int64_t part_floats, unsigned* guard, int wx3_taps, void* stream) {
+                        int64_t part_floats, unsigned* guard, int wx3_taps, int nprod, void* stream) {
   return conv_x3_run(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, wx3_taps,
-                     nullptr, 0, nullptr, nullptr, stream);
+                     nullptr, 0, nullptr, nullptr, nprod, stream);
 }
 
 int64_t ifd_tr_gstat_floats(int N, int H, int cout) {
@@ -1802,9 +1815,9 @@ int64_t ifd_tr_gstat_floats(int N, int H, int cout) {
 int ifd_tr_conv_x3_gstat(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
                          const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
                          int64_t part_floats, unsigned* guard, int taps, float* gstat, int64_t gstat_floats,
-                         int* gstat_E, float* gstat_cnt, void* stream) {
+                         int* gstat_E, float* gstat_cnt, int nprod, void* stream) {
   return conv_x3_run(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, taps,
-                     gstat, gstat_floats, gstat_E, gstat_cnt, stream);
+                     gstat, gstat_floats, gstat_E, gstat_cnt, nprod, stream);
 }
 
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream) {
@@ -1875,7 +1888,7 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
 
 int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                          int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
-                         int64_t colpart_floats, unsigned* guard, void* stream) {
+                         int64_t colpart_floats, unsigned* guard, int nprod, void* stream) {
   // the split kernel: 3x3 or 1x1, one input tensor, power-of-two maps >= 8, channel counts in 16-B quads
   // (its staging loads four channels at a time); else fp32
   // (and images within a buffer descriptor's 2 GB range: the staging loads address one image each)
@@ -1886,7 +1899,7 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   const int64_t P = (int64_t)N * H * H;
   int S = 1;
   const int64_t need = ifd_tr_wgrad_part_floats(cout, c0, taps, P, &S);
-  if (!dy || !x0 || !dw || !part || need > part_floats) {
+  if (!dy || !x0 || !dw || !part || need > part_floats || (nprod != 1 && nprod != 3)) {
     set_error("ifd_tr_conv_wgrad_x3: bad arguments or workspace too small");
     return 2;
   }
@@ -1900,12 +1913,15 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   const int tiles = ((cout + 63) / 64) * ((c0 + 63) / 64);
   // bias gradient fused into the kernel when the column-sum workspace holds one row per split
   const bool fused_db = db && colpart && (int64_t)S * cout <= colpart_floats && cout % 4 == 0;
-  if (taps == 9)
-    hipLaunchKernelGGL(wgrad_x3_kernel<9>, dim3(tiles, S), dim3(WxCfg<9>::NT), 0, s, a, guard,
-                       fused_db ? colpart : nullptr);
+  float* cp = fused_db ? colpart : nullptr;
+  if (taps == 9 && nprod == 3)
+    hipLaunchKernelGGL((wgrad_x3_kernel<9, 3>), dim3(tiles, S), dim3(WxCfg<9>::NT), 0, s, a, guard, cp);
+  else if (taps == 9)
+    hipLaunchKernelGGL((wgrad_x3_kernel<9, 1>), dim3(tiles, S), dim3(WxCfg<9>::NT), 0, s, a, guard, cp);
+  else if (nprod == 3)
+    hipLaunchKernelGGL((wgrad_x3_kernel<1, 3>), dim3(tiles, S), dim3(WxCfg<1>::NT), 0, s, a, guard, cp);
   else
-    hipLaunchKernelGGL(wgrad_x3_kernel<1>, dim3(tiles, S), dim3(WxCfg<1>::NT), 0, s, a, guard,
-                       fused_db ? colpart : nullptr);
+    hipLaunchKernelGGL((wgrad_x3_kernel<1, 1>), dim3(tiles, S), dim3(WxCfg<1>::NT), 0, s, a, guard, cp);
   const int64_t n = (int64_t)cout * c0 * taps;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (fused_db) {

@@ -37,16 +37,16 @@ TRAIN_EXPORTS = {
     "ifd_tr_pack_conv_x3": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "ifd_tr_conv_x3_part_floats": (i64, [i32, i32, i32, i32]),
     "ifd_tr_conv_x3": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, vp]),
-    "ifd_tr_conv_x3_taps": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp]),
+    "ifd_tr_conv_x3_taps": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, i32, vp]),
     "ifd_tr_gstat_floats": (i64, [i32, i32, i32]),
     "ifd_tr_conv_x3_gstat": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, i64,
-                                   vp, vp, vp]),
+                                   vp, vp, i32, vp]),
     "ifd_tr_gn_fwd_gstat": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, i32, vp, i32, f32, vp, vp, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
     "ifd_tr_conv_wgrad": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp]),
-    "ifd_tr_conv_wgrad_x3": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp, vp]),
+    "ifd_tr_conv_wgrad_x3": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, vp, i64, vp, i64, vp, i32, vp]),
     "ifd_tr_gn_fwd": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_gn_bwd": (i32, [vp, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, i64, vp]),
     "ifd_tr_resample": (i32, [vp, i32, i32, i32, i32, vp, vp]),
@@ -107,13 +107,21 @@ class UNetTrainer:
     2^x3_loss_scale_log2 (the eps-MSE gradient is ~1e-7 per element: below f16's normal range unscaled);
     every backward op is linear in the upstream gradient and the scale is a power of two, so removing it
     from the parameter gradients before clip + AdamW is exact. A split operand outside f16's range sets
-    the range guard; the step is then recomputed in fp32 (same noise) with a warning. wgrad, GroupNorm,
-    attention, embeddings, the 1x1 convs and the optimizer stay fp32."""
+    the range guard; the step is then recomputed in fp32 (same noise) with a warning. GroupNorm, attention,
+    embeddings and the optimizer stay fp32.
+
+    precision="f16": the reduced-precision variant of the same path (BASELINE configs[4] names a bf16 fine-tune,
+    which the reference has no code for): the split kernels with ONE product per MAC (f16 operands, fp32
+    accumulation) for the forward, dgrad and weight-gradient convs, the same loss scale and range guard.
+    Not fp32-class: reported separately, checked against the fp32 step at a stated tolerance
+    (tests/test_gpu_train.py::test_train_f16_full_vs_fp32)."""
+
+    SPLIT_MODES = ("3xf16", "f16")
 
     def __init__(self, cfg: UNetConfig = FULL, device="cuda", lr=5e-5, weight_decay=0.01, betas=(0.9, 0.999),
                  eps=1e-8, max_norm=1.0, precision="fp32", x3_dgrad=True, x3_wgrad=True, x3_loss_scale_log2=20):
-        if precision not in ("fp32", "3xf16"):
-            raise ValueError(f"precision must be 'fp32' or '3xf16', got {precision!r}")
+        if precision not in ("fp32", "3xf16", "f16"):
+            raise ValueError(f"precision must be 'fp32', '3xf16' or 'f16', got {precision!r}")
         self.precision = precision
         self.x3_dgrad = bool(x3_dgrad)
         self.x3_wgrad = bool(x3_wgrad)
@@ -203,8 +211,14 @@ class UNetTrainer:
             self._pack_cache[key] = buf
         return buf, pout, pin, taps, bn, cin_pad, cout_pad
 
+    def _split(self):
+        return self.precision in self.SPLIT_MODES
+
+    def _nprod(self):
+        return 1 if self.precision == "f16" else 3
+
     def _x3_active(self, transpose):
-        return self.precision == "3xf16" and (not transpose or self.x3_dgrad)
+        return self._split() and (not transpose or self.x3_dgrad)
 
     def _conv_x3(self, x, cin_x, N, H, name, bias_name, res, x1, c1, transpose):
         """The conv on the 3xf16 split kernel, or None when its shape is not eligible (fp32 kernel then)."""
@@ -247,12 +261,12 @@ class UNetTrainer:
             E, cnt = _c.c_int(0), _c.c_float(0.0)
             rc = lib().ifd_tr_conv_x3_gstat(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, ppad, P(res), P(out),
                                             P(part), pf, P(self._guard), taps, P(gstat), gf, _c.byref(E),
-                                            _c.byref(cnt), self.s)
+                                            _c.byref(cnt), self._nprod(), self.s)
             if rc == 0 and E.value > 0:
                 self._gstat[out.data_ptr()] = (out, gstat, E.value, cnt.value, pout, None)
         else:
             rc = lib().ifd_tr_conv_x3_taps(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, ppad, P(res), P(out),
-                                           P(part), pf, P(self._guard), taps, self.s)
+                                           P(part), pf, P(self._guard), taps, self._nprod(), self.s)
         if rc == 3:
             return None
         chk(rc)
@@ -299,9 +313,9 @@ class UNetTrainer:
         direct = real_cin == cin_x and real_cout == cout
         dw = self.g(name) if direct else self._zeros(cout * cin_x * taps)
         db = self.g(bias_name) if (bias_name and real_cout == cout) else (self._zeros(cout) if bias_name else None)
-        if self.precision == "3xf16" and self.x3_wgrad:
+        if self._split() and self.x3_wgrad:
             chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
-                                           P(colpart), colpart.numel(), P(self._guard), self.s))
+                                           P(colpart), colpart.numel(), P(self._guard), self._nprod(), self.s))
         else:
             chk(lib().ifd_tr_conv_wgrad(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
                                         P(colpart), colpart.numel(), self.s))
@@ -638,7 +652,7 @@ class UNetTrainer:
         chk(lib().ifd_tr_masked_mse(P(out6), cs, P(nc_), P(mc), N, H * W, P(self.loss), P(self._dout6), P(work),
                                     self.s))
         self._gscale = 1.0
-        if self.precision == "3xf16" and (self.x3_dgrad or self.x3_wgrad):
+        if self._split() and (self.x3_dgrad or self.x3_wgrad):
             self._gscale = float(2.0 ** self.x3_loss_scale_log2)
             chk(lib().ifd_tr_scale(P(self._dout6), self._dout6.numel(), self._gscale, self.s))
         return self.loss
@@ -659,26 +673,26 @@ class UNetTrainer:
     def train_step(self, diffusion, images, masked_images, masks, t, noise=None, noise_device=None):
         """One iteration of train_epoch (code/train_inpainting.py:27-66): zero_grad, training_losses,
         backward, clip_grad_norm_(1.0), AdamW.step(). Returns the loss as a device scalar.
-        3xf16: one host read of the range guard per step; a trip recomputes the step in fp32."""
+        3xf16 / f16: one host read of the range guard per step; a trip recomputes the step in fp32."""
         self.zero_grad()
-        if self.precision == "3xf16":
+        if self._split():
             self._guard.zero_()
         loss = self.training_loss(diffusion, images, t, {"masked_image": masked_images, "mask": masks}, noise=noise,
                                   noise_device=noise_device)
         self.backward(self._dout6)
-        if self.precision == "3xf16" and int(self._guard[0].item()):
+        if self._split() and int(self._guard[0].item()):
             import warnings
-            warnings.warn("3xf16 range guard tripped (an operand or weight outside the f16 split's range): "
-                          "step recomputed in fp32")
+            warnings.warn(f"{self.precision} range guard tripped (an operand or weight outside the f16 split's "
+                          "range): step recomputed in fp32")
             self.guard_trips += 1
-            self.precision = "fp32"
+            prec, self.precision = self.precision, "fp32"
             try:
                 self.zero_grad()
                 xt, mi, mc, nc_, _x0, tt = self._keep
                 loss = self._forward_loss(xt, tt, mi, mc, nc_)
                 self.backward(self._dout6)
             finally:
-                self.precision = "3xf16"
+                self.precision = prec
         self.optimizer_step()
         return loss
 

@@ -48,10 +48,11 @@ int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int 
                    int cin_pad, int cout, const float* res, float* out, float* part, int64_t part_floats,
                    unsigned* guard, void* stream);
 /* ifd_tr_conv_x3 for 3x3 (taps 9) or 1x1 (taps 1: cin % 32 == 0, weights packed by ifd_tr_pack_conv_x3 with
- * taps 1, part size from ifd_tr_conv_x3_part_floats). */
+ * taps 1, part size from ifd_tr_conv_x3_part_floats). nprod: 3 (the fp32-class split) or 1 (the reduced-
+ * precision f16 training mode: the hi x hi product only, same packing). */
 int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
                         const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
-                        int64_t part_floats, unsigned* guard, int taps, void* stream);
+                        int64_t part_floats, unsigned* guard, int taps, int nprod, void* stream);
 /* ifd_tr_conv_x3_taps that also writes the output's GroupNorm granule statistics when the launch geometry
  * has them (cout % 128 == 0; single-image 256-pixel tiles or a split-K reduction): gstat[n][cout/4][E] =
  * (mean, M2) of *gstat_cnt values each; *gstat_E = E, or 0 when none were written (then use ifd_tr_gn_fwd).
@@ -61,7 +62,7 @@ int64_t ifd_tr_gstat_floats(int N, int H, int cout);
 int ifd_tr_conv_x3_gstat(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
                          const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
                          int64_t part_floats, unsigned* guard, int taps, float* gstat, int64_t gstat_floats,
-                         int* gstat_E, float* gstat_cnt, void* stream);
+                         int* gstat_E, float* gstat_cnt, int nprod, void* stream);
 /* x[i] *= s (the loss scale of the 3xf16 backward and its removal from the gradients). */
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream);
 /* dw[cout][c0+c1][taps] += sum_pixels dy (x) shifted concat(x0, x1); db[cout] += column sums of dy. */
@@ -71,10 +72,11 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
                       int64_t colpart_floats, void* stream);
 /* ifd_tr_conv_wgrad with the 3xf16 split kernel for 3x3 convs of one input tensor on maps >= 8x8 (both
  * operands split on the fly, three f16 products per MAC, fp32 accumulation; |operand| >= 65504 sets bit 1
- * of *guard); other shapes run ifd_tr_conv_wgrad. Same workspaces. */
+ * of *guard); other shapes run ifd_tr_conv_wgrad. Same workspaces. nprod 1: the hi x hi product only (the
+ * reduced-precision f16 training mode). */
 int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                          int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
-                         int64_t colpart_floats, unsigned* guard, void* stream);
+                         int64_t colpart_floats, unsigned* guard, int nprod, void* stream);
 /* GroupNorm(32, C) (+ scale/shift: ss[n][0:C] = scale, ss[n][C:2C] = shift, row stride ss_stride) (+ SiLU).
  * stats[n][32][2] = (mean, rstd) saved for the backward; work: N * ceil(HW/256) * 64 doubles. */
 int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,

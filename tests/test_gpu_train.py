@@ -232,3 +232,34 @@ def test_train_x3_head_dgrad_fallback(record):
     record("train_x3_head_dgrad_fallback_vs_fp32", rel_loss=abs(l3 - l32) / abs(l32), max_tensor_grad_rel=worst)
     assert abs(l3 - l32) <= 1e-5 * abs(l32)
     assert worst <= 1e-4
+
+
+def test_train_f16_full_vs_fp32(record):
+    """The reduced-precision training variant (precision="f16": the split kernels with one f16 product per
+    MAC for the forward, dgrad and weight-gradient convs; fp32 accumulation, loss scale 2^20) against the
+    fp32 step from the same state at full size, B = 4. Not fp32-class; the tolerances stated here: loss
+    relative 1e-3, global grad norm relative 1e-2, every parameter gradient rel-L2 <= 5e-2, no guard trip."""
+    tr32, l32 = _full_step("fp32")
+    g32 = tr32.grad.clone()
+    n32 = float(tr32.norm_coef[0])
+    offs = tr32.offsets
+    del tr32
+    tr16, l16 = _full_step("f16")
+    assert tr16.guard_trips == 0
+    rel_loss = abs(l16 - l32) / abs(l32)
+    rel_gn = abs(float(tr16.norm_coef[0]) - n32) / n32
+    worst, wname, rels = 0.0, None, []
+    for k, (o, shape) in offs.items():
+        n = int(np.prod(shape))
+        a, b = tr16.grad[o:o + n].double(), g32[o:o + n].double()
+        bn = float(b.norm())
+        if bn == 0.0:
+            continue
+        r = float((a - b).norm()) / bn
+        rels.append(r)
+        if r > worst:
+            worst, wname = r, k
+    record("train_f16_full_vs_fp32", loss=l16, loss_fp32=l32, rel_loss=rel_loss, rel_grad_norm=rel_gn,
+           max_tensor_grad_rel=worst, median_tensor_grad_rel=float(np.median(rels)), worst_tensor=wname)
+    assert rel_loss <= 1e-3 and rel_gn <= 1e-2, (rel_loss, rel_gn)
+    assert worst <= 5e-2, (worst, wname)

@@ -43,7 +43,7 @@ def _conv(N, H, cin, cout, res, seed):
     out = torch.empty(N, H, H, cout, device=DEV)
     E, cnt = ctypes.c_int(0), ctypes.c_float(0.0)
     chk(lib().ifd_tr_conv_x3_gstat(P(x), cin, None, 0, N, H, P(wx3), P(b), cin, cout, P(r), P(out), P(part), pf,
-                                   P(guard), 9, P(gstat), gf, ctypes.byref(E), ctypes.byref(cnt), s))
+                                   P(guard), 9, P(gstat), gf, ctypes.byref(E), ctypes.byref(cnt), 3, s))
     return out, gstat, E.value, cnt.value
 
 

@@ -21,7 +21,7 @@ P = T.P
 def run(x3):
     if x3:
         return T.lib().ifd_tr_conv_wgrad_x3(P(dy), C, P(x), C, None, 0, N, H, 9, P(dw), P(db), P(part), need, P(colpart),
-                                            colpart.numel(), P(guard), ctypes.c_void_p(s))
+                                            colpart.numel(), P(guard), 3, ctypes.c_void_p(s))
     return T.lib().ifd_tr_conv_wgrad(P(dy), C, P(x), C, None, 0, N, H, 9, P(dw), P(db), P(part), need, P(colpart),
                                      colpart.numel(), ctypes.c_void_p(s))
 for x3 in (0, 1):
