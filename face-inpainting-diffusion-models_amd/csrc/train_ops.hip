@@ -77,6 +77,9 @@ struct WgArgs {
   int64_t P;           // N * H * W
   int chunks_per_split;
   float* part;         // [S][cout][cin][taps]
+  // wgrad_x3_kernel<.., GNA = true>: X = silu(actA[n][c] x + actB[n][c]) of the raw x0, zero padded after the
+  // activation (the forward conv's GroupNorm + SiLU prologue, recomputed at staging instead of materialised)
+  const float* actA; const float* actB;
 };
 
 __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs a) {
@@ -394,7 +397,9 @@ struct WxCfg {
 // TAPS = 9 (3x3, halo of one pixel) or 1 (1x1: the chunk's own pixels, no halo).
 // NPROD = 3 (fp32-class: three split products) or 1 (the reduced-precision f16 training mode: the hi x hi
 // product only; no lo planes are staged or read).
-template <int TAPS, int NPROD>
+// GNA: the X operand is the GroupNorm-applied, SiLU-activated raw input (WgArgs::actA / actB), computed
+// per staged value exactly as conv_x3.hip's producers compute it for the forward conv.
+template <int TAPS, int NPROD, bool GNA>
 __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
   using Cf = WxCfg<TAPS>;
   constexpr int NT = Cf::NT, WX_DI = Cf::DI, WX_XI = Cf::XI, NTMAX = Cf::NTMAX;
@@ -439,6 +444,8 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
     const bool co_ok = co0 + 4 * cq + 3 < a.cout, ci_ok = ci0 + 4 * cq + 3 < cin;
     // two register sets (chunk parity): a chunk's loads go out two chunks before its staging
     f32x4 dvs[2][WX_DI], xvs[2][WX_XI];
+    f32x4 gas[GNA ? 2 : 1], gbs[GNA ? 2 : 1];  // GNA: the chunk's image's coefficients of the thread's quad
+    unsigned okm[GNA ? 2 : 1];                 // GNA: bit k = halo item k inside the map (else padding)
     int xhy[WX_XI], xhx[WX_XI], ld_x[WX_XI], ld_d[WX_DI];
 #pragma unroll
     for (int k = 0; k < WX_XI; ++k) {
@@ -475,11 +482,20 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       const int ox = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * cin * 4);
 #pragma unroll
       for (int k = 0; k < WX_DI; ++k) dv[k] = bld4(rd, co_ok ? ld_d[k] + od : WX_OOB, 0);
+      unsigned m = 0;
 #pragma unroll
       for (int k = 0; k < WX_XI; ++k) {
         const int y = y0 + xhy[k], x = x0 + xhx[k];
         const bool ok = ci_ok & ((unsigned)y < (unsigned)a.H) & ((unsigned)x < (unsigned)a.W);  // (no branches)
         xv[k] = bld4(rx, ok ? ld_x[k] + ox : WX_OOB, 0);
+        m |= ok ? 1u << k : 0u;
+      }
+      if constexpr (GNA) {
+        constexpr int S = decltype(SETc)::value;
+        okm[S] = m;
+        const int oc = ci_ok ? (ci0 + 4 * cq) * 4 : WX_OOB;
+        gas[S] = bld4(mkrsrc(a.actA + (size_t)n * cin), oc, 0);
+        gbs[S] = bld4(mkrsrc(a.actB + (size_t)n * cin), oc, 0);
       }
     };
     // staging of one chunk in WX_PARTS slices (items: the WX_DI dY quads, then the WX_XI halo quads), so
@@ -493,9 +509,20 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
         if (it >= WX_ITEMS) return;
         const bool isd = it < WX_DI;
         const int k = isd ? it : it - WX_DI;
-        const f32x4 v = isd ? dv[k] : xv[k];
+        f32x4 v = isd ? dv[k] : xv[k];
         const int row = (tid + NT * k) >> 4;
         if (!isd && row >= HP) return;
+        if constexpr (GNA) {
+          if (!isd) {  // conv_x3.hip's prologue: padding rides in the exponent (2^+inf -> rcp -> 0)
+            constexpr int S = decltype(SETc)::value;
+            const float pinf = (okm[S] >> k) & 1u ? 0.f : __builtin_inff();
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float t = fmaf(gas[S][j], v[j], gbs[S][j]);
+              v[j] = t * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(fmaf(t, -1.4426950408889634f, pinf)));
+            }
+          }
+        }
         if (isd && do_cs) csum += v;
         unsigned h0, l0, h1, l1;
         wx_split2(v[0], v[1], h0, l0);
@@ -782,9 +809,33 @@ __global__ __launch_bounds__(256) void gn_stat_partial_kernel(const float* __res
 // split-K reduction's): channels [0, C0) from g0[n][C0/4][E], [C0, C) from g1[n][(C-C0)/4][E] (a
 // concat's two sources) as (mean, M2). One wave per (n, g), float64 merges in a fixed order (mean of
 // the means, then M2 = sum M2_i + cnt sum (mean_i - mean)^2)
+// Optional per-channel coefficients of the GroupNorm apply (GnCoef::A non-null): A = rstd gamma (1 + s),
+// B = (beta - mean rstd gamma)(1 + s) + shift, so that act(A x + B) is the normalised activation the
+// convs' prologues (and the split weight gradient's staging) compute on load; the arithmetic of
+// norm.hip's gn_finalize2 (the sampler's coefficients).
+struct GnCoef {
+  const float* gamma; const float* beta; const float* ss; int ss_stride;
+  float* A; float* B;  // [N][C]
+};
+__device__ __forceinline__ void gn_coef_write(const GnCoef& k, int n, int g, int C, float meanf, float rstd) {
+  const int cpg = C / 32;
+  for (int j = threadIdx.x; j < cpg; j += 64) {
+    const int c = g * cpg + j;
+    const float a = rstd * k.gamma[c];
+    const float b = k.beta[c] - meanf * a;
+    float A = a, B = b;
+    if (k.ss) {
+      const float sc = 1.0f + k.ss[(int64_t)n * k.ss_stride + c];
+      A = a * sc;
+      B = b * sc + k.ss[(int64_t)n * k.ss_stride + C + c];
+    }
+    k.A[(int64_t)n * C + c] = A;
+    k.B[(int64_t)n * C + c] = B;
+  }
+}
 __global__ __launch_bounds__(64) void gn_granule_final_kernel(const float* __restrict__ g0, int C0,
                                                               const float* __restrict__ g1, int E, float cnt, int C,
-                                                              float* __restrict__ stats) {
+                                                              float* __restrict__ stats, GnCoef coef) {
   const int i = blockIdx.x;  // (n, g)
   const int n = i / 32, g = i % 32;
   const int qpg = C / 128;   // channel quads per group
@@ -807,15 +858,18 @@ __global__ __launch_bounds__(64) void gn_granule_final_kernel(const float* __res
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
-  if (threadIdx.x) return;
   double var = q / ((double)K * cnt);
   if (var < 0) var = 0;
-  stats[i * 2] = (float)mean;
-  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+  // (lane 0's values everywhere: the butterflies' sums can differ between lanes in the last bit)
+  const float meanf = __shfl((float)mean, 0), rstd = __shfl((float)(1.0 / sqrt(var + 1e-5)), 0);
+  if (coef.A) gn_coef_write(coef, n, g, C, meanf, rstd);
+  if (threadIdx.x) return;
+  stats[i * 2] = meanf;
+  stats[i * 2 + 1] = rstd;
 }
 // one wave per (n, g): the lanes stride the slices, then a fixed butterfly (deterministic)
 __global__ __launch_bounds__(64) void gn_stat_final_kernel(const double* __restrict__ part, int nsl, int HW, int C,
-                                                           int N, float* __restrict__ stats) {
+                                                           int N, float* __restrict__ stats, GnCoef coef) {
   const int i = blockIdx.x;  // (n, g)
   const int n = i / 32, g = i % 32;
   double a = 0.0, b = 0.0;
@@ -828,13 +882,16 @@ __global__ __launch_bounds__(64) void gn_stat_final_kernel(const double* __restr
     a += __shfl_xor(a, off);
     b += __shfl_xor(b, off);
   }
-  if (threadIdx.x) return;
   const double cnt = (double)HW * (C / 32);
   const double mean = a / cnt;
   double var = b / cnt - mean * mean;
   if (var < 0) var = 0;
-  stats[i * 2] = (float)mean;
-  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+  // (lane 0's values everywhere: the butterflies' sums can differ between lanes in the last bit)
+  const float meanf = __shfl((float)mean, 0), rstd = __shfl((float)(1.0 / sqrt(var + 1e-5)), 0);
+  if (coef.A) gn_coef_write(coef, n, g, C, meanf, rstd);
+  if (threadIdx.x) return;
+  stats[i * 2] = meanf;
+  stats[i * 2 + 1] = rstd;
 }
 
 __device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + expf(-z)); }
@@ -1682,6 +1739,32 @@ int ifd_tr_conv(const float* x0, int c0, const float* x1, int c1, int N, int H, 
   return e;
 }
 
+int ifd_tr_conv_gn(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* wpack,
+                   const float* bias, int cin_pad, int cout, int cout_pad, int bn, int taps, const float* actA,
+                   const float* actB, const float* res, float* out, float* part, int64_t part_floats, void* stream) {
+  if ((H & (H - 1)) || c0 % 8 || c1 % 8 || c0 + c1 != cin_pad || (bn != 32 && bn != 64) || cout_pad % bn ||
+      cout % 4 || cout > cout_pad || (taps != 1 && taps != 9) || !x0 || !out || !wpack || !bias || !actA || !actB) {
+    set_error("ifd_tr_conv_gn: unsupported arguments");
+    return 2;
+  }
+  ConvParams p;
+  conv_params(p, x0, c0, c1 ? x1 : nullptr, c1, N, H, wpack, bias, cin_pad, cout, cout_pad, bn, taps, res, out);
+  p.act = ACT_AFFINE_SILU;
+  p.actA = actA;
+  p.actB = actB;
+  if (p.ksplit > 1) {
+    if (!part || (int64_t)p.ksplit * N * H * H * cout > part_floats) {
+      set_error("ifd_tr_conv_gn: split-K workspace too small (ifd_tr_conv_part_floats)");
+      return 2;
+    }
+    p.part = part;
+  }
+  int e = launch_conv(p, taps, XF_NONE, bn, (hipStream_t)stream);
+  if (!e && p.ksplit > 1) e = launch_splitk_reduce(p, (hipStream_t)stream);
+  if (e) set_error(std::string("ifd_tr_conv_gn: ") + hipGetErrorString((hipError_t)e));
+  return e;
+}
+
 int ifd_tr_pack_conv_x3(const float* w, int cout, int cin, int taps, int cin_pad16, int cout_pad, int transpose,
                         void* wx3, unsigned* guard, void* stream) {
   if (!w || !wx3 || !guard || (taps != 9 && taps != 1) || cin_pad16 % (taps == 1 ? 32 : 16) || cout_pad % 64) {
@@ -1738,7 +1821,8 @@ int ifd_tr_conv_x3(const float* x0, int c0, const float* x1, int c1, int N, int 
 static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
                        const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
                        int64_t part_floats, unsigned* guard, int wx3_taps, float* gstat, int64_t gstat_floats,
-                       int* gstat_E, float* gstat_cnt, int nprod, void* stream) {
+                       int* gstat_E, float* gstat_cnt, int nprod, void* stream, const float* actA = nullptr,
+                       const float* actB = nullptr) {
   if (gstat_E) *gstat_E = 0;
   if ((H & (H - 1)) || c0 + c1 != cin_pad || !x0 || !out || !wx3 || !bias || !guard || (nprod != 1 && nprod != 3)) {
     set_error("ifd_tr_conv_x3: unsupported arguments");
@@ -1750,9 +1834,18 @@ static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, 
     set_error("ifd_tr_conv_x3: 1x1 needs one input with cin % 32 == 0");
     return 3;
   }
+  if (actA && (taps != 9 || !actB)) {  // (the 1x1 operand goes to LDS by DMA, unactivated)
+    set_error("ifd_tr_conv_x3_gn: the GroupNorm prologue needs a 3x3 conv and both coefficient arrays");
+    return 3;
+  }
   conv_x3_params(p, x0, c0, c1 ? x1 : nullptr, c1, N, H, wx3, bias, cin_pad, cout, res, out, taps);
   p.guard = guard;
   p.x3_nprod = nprod;
+  if (actA) {
+    p.act = ACT_AFFINE_SILU;
+    p.actA = actA;
+    p.actB = actB;
+  }
   const int nct = cout / 64;  // the non-SKIP split kernel decodes channel tiles by shifts
   if (cout % 64 || (taps == 9 && (nct & (nct - 1))) || !conv_x3_eligible(p, taps, XF_NONE, 64)) {
     set_error("ifd_tr_conv_x3: shape not eligible for the split kernel (use ifd_tr_conv)");
@@ -1804,6 +1897,14 @@ int ifd_tr_conv_x3_taps(const float* x0, int c0, const float* x1, int c1, int N,
                         int64_t part_floats, unsigned* guard, int wx3_taps, int nprod, void* stream) {
   return conv_x3_run(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, wx3_taps,
                      nullptr, 0, nullptr, nullptr, nprod, stream);
+}
+
+int ifd_tr_conv_x3_gn(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
+                      const float* bias, int cin_pad, int cout, const float* actA, const float* actB, const float* res,
+                      float* out, float* part, int64_t part_floats, unsigned* guard, float* gstat,
+                      int64_t gstat_floats, int* gstat_E, float* gstat_cnt, int nprod, void* stream) {
+  return conv_x3_run(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, 9, gstat,
+                     gstat_floats, gstat_E, gstat_cnt, nprod, stream, actA, actB);
 }
 
 int64_t ifd_tr_gstat_floats(int N, int H, int cout) {
@@ -1886,6 +1987,10 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
   return TR_LAST();
 }
 
+static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int N, int H, int taps,
+                        const float* actA, const float* actB, float* dw, float* db, float* part, int64_t part_floats,
+                        float* colpart, int64_t colpart_floats, unsigned* guard, int nprod, void* stream);
+
 int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                          int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
                          int64_t colpart_floats, unsigned* guard, int nprod, void* stream) {
@@ -1896,6 +2001,25 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
       (int64_t)H * H * (cout > c0 ? cout : c0) * 4 >= 0x7ffffff0)
     return ifd_tr_conv_wgrad(dy, cout, x0, c0, x1, c1, N, H, taps, dw, db, part, part_floats, colpart, colpart_floats,
                              stream);
+  return wgrad_x3_run(dy, cout, x0, c0, N, H, taps, nullptr, nullptr, dw, db, part, part_floats, colpart,
+                      colpart_floats, guard, nprod, stream);
+}
+
+int ifd_tr_conv_wgrad_x3_gn(const float* dy, int cout, const float* x0, int c0, int N, int H, const float* actA,
+                            const float* actB, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
+                            int64_t colpart_floats, unsigned* guard, int nprod, void* stream) {
+  if (!actA || !actB || H < 8 || (H & (H - 1)) || !guard || cout % 4 || c0 % 4 ||
+      (int64_t)H * H * (cout > c0 ? cout : c0) * 4 >= 0x7ffffff0) {
+    set_error("ifd_tr_conv_wgrad_x3_gn: shape not eligible for the split kernel (materialise the activation)");
+    return 3;
+  }
+  return wgrad_x3_run(dy, cout, x0, c0, N, H, 9, actA, actB, dw, db, part, part_floats, colpart, colpart_floats,
+                      guard, nprod, stream);
+}
+
+static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int N, int H, int taps,
+                        const float* actA, const float* actB, float* dw, float* db, float* part, int64_t part_floats,
+                        float* colpart, int64_t colpart_floats, unsigned* guard, int nprod, void* stream) {
   const int64_t P = (int64_t)N * H * H;
   int S = 1;
   const int64_t need = ifd_tr_wgrad_part_floats(cout, c0, taps, P, &S);
@@ -1907,6 +2031,7 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   a.dy = dy; a.cout = cout; a.x0 = x0; a.c0 = c0; a.x1 = x0; a.c1 = 0;
   a.N = N; a.H = H; a.W = H; a.taps = taps; a.P = P;
   a.part = part;
+  a.actA = actA; a.actB = actB;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nch = P / WX_PX;
   a.chunks_per_split = (int)((nch + S - 1) / S);
@@ -1914,14 +2039,20 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   // bias gradient fused into the kernel when the column-sum workspace holds one row per split
   const bool fused_db = db && colpart && (int64_t)S * cout <= colpart_floats && cout % 4 == 0;
   float* cp = fused_db ? colpart : nullptr;
-  if (taps == 9 && nprod == 3)
-    hipLaunchKernelGGL((wgrad_x3_kernel<9, 3>), dim3(tiles, S), dim3(WxCfg<9>::NT), 0, s, a, guard, cp);
+  const bool gna = actA != nullptr;
+  const dim3 g9(tiles, S), b9(WxCfg<9>::NT), b1(WxCfg<1>::NT);
+  if (taps == 9 && nprod == 3 && gna)
+    hipLaunchKernelGGL((wgrad_x3_kernel<9, 3, true>), g9, b9, 0, s, a, guard, cp);
+  else if (taps == 9 && nprod == 3)
+    hipLaunchKernelGGL((wgrad_x3_kernel<9, 3, false>), g9, b9, 0, s, a, guard, cp);
+  else if (taps == 9 && gna)
+    hipLaunchKernelGGL((wgrad_x3_kernel<9, 1, true>), g9, b9, 0, s, a, guard, cp);
   else if (taps == 9)
-    hipLaunchKernelGGL((wgrad_x3_kernel<9, 1>), dim3(tiles, S), dim3(WxCfg<9>::NT), 0, s, a, guard, cp);
+    hipLaunchKernelGGL((wgrad_x3_kernel<9, 1, false>), g9, b9, 0, s, a, guard, cp);
   else if (nprod == 3)
-    hipLaunchKernelGGL((wgrad_x3_kernel<1, 3>), dim3(tiles, S), dim3(WxCfg<1>::NT), 0, s, a, guard, cp);
+    hipLaunchKernelGGL((wgrad_x3_kernel<1, 3, false>), g9, b1, 0, s, a, guard, cp);
   else
-    hipLaunchKernelGGL((wgrad_x3_kernel<1, 1>), dim3(tiles, S), dim3(WxCfg<1>::NT), 0, s, a, guard, cp);
+    hipLaunchKernelGGL((wgrad_x3_kernel<1, 1, false>), g9, b1, 0, s, a, guard, cp);
   const int64_t n = (int64_t)cout * c0 * taps;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (fused_db) {
@@ -1950,7 +2081,7 @@ int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, cons
   }
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gn_stat_partial_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, work);
-  hipLaunchKernelGGL(gn_stat_final_kernel, dim3(N * 32), dim3(64), 0, s, work, nsl, HW, C, N, stats);
+  hipLaunchKernelGGL(gn_stat_final_kernel, dim3(N * 32), dim3(64), 0, s, work, nsl, HW, C, N, stats, GnCoef{});
   hipLaunchKernelGGL(gn_apply_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, stats, gamma, beta, ss,
                      ss_stride, act_silu, out);
   return TR_LAST();
@@ -1965,11 +2096,48 @@ int ifd_tr_gn_fwd_gstat(const float* x, int N, int HW, int C, const float* gamma
     return 2;
   }
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gn_granule_final_kernel, dim3(N * 32), dim3(64), 0, s, gstat0, C0, gstat1, E, cnt, C, stats);
+  hipLaunchKernelGGL(gn_granule_final_kernel, dim3(N * 32), dim3(64), 0, s, gstat0, C0, gstat1, E, cnt, C, stats,
+                     GnCoef{});
   const int nsl = (HW + GN_SL - 1) / GN_SL;
   hipLaunchKernelGGL(gn_apply_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, stats, gamma, beta, ss, ss_stride,
                      act_silu, out);
   return TR_LAST();
+}
+
+int ifd_tr_gn_coef(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
+                   int ss_stride, const float* gstat0, int C0, const float* gstat1, int E, float cnt, float* stats,
+                   float* A, float* B, double* work, int64_t work_doubles, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const GnCoef k{gamma, beta, ss, ss_stride, A, B};
+  if (!A || !B || !gamma || !beta || C % 32 || C > 1024) {
+    set_error("ifd_tr_gn_coef: C must be a multiple of 32 (<= 1024); A, B, gamma, beta required");
+    return 2;
+  }
+  if (gstat0) {
+    if (C % 128 || C0 % 4 || C0 <= 0 || C0 > C || (C0 < C && !gstat1) || E <= 0 || (double)E * cnt != 4.0 * HW) {
+      set_error("ifd_tr_gn_coef: granules need C % 128 == 0, 0 < C0 <= C in quads, E * cnt == 4 * HW");
+      return 2;
+    }
+    hipLaunchKernelGGL(gn_granule_final_kernel, dim3(N * 32), dim3(64), 0, s, gstat0, C0, gstat1, E, cnt, C, stats, k);
+    return TR_LAST();
+  }
+  const int nsl = (HW + GN_SL - 1) / GN_SL;
+  if (!x || (int64_t)N * nsl * 64 > work_doubles) {
+    set_error("ifd_tr_gn_coef: work >= N * ceil(HW/256) * 64 doubles");
+    return 2;
+  }
+  hipLaunchKernelGGL(gn_stat_partial_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, work);
+  hipLaunchKernelGGL(gn_stat_final_kernel, dim3(N * 32), dim3(64), 0, s, work, nsl, HW, C, N, stats, k);
+  return TR_LAST();
+}
+
+int ifd_tr_act_apply(const float* x, int N, int HW, int C, const float* A, const float* B, int silu, float* out,
+                     void* stream) {
+  if (!x || !A || !B || !out || C % 4) {
+    set_error("ifd_tr_act_apply: bad arguments");
+    return 2;
+  }
+  return launch_act_apply(x, C, N, HW, silu ? ACT_AFFINE_SILU : ACT_AFFINE, A, B, out, (hipStream_t)stream);
 }
 
 int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,

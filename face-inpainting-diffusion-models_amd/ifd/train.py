@@ -42,6 +42,13 @@ TRAIN_EXPORTS = {
     "ifd_tr_conv_x3_gstat": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, i64,
                                    vp, vp, i32, vp]),
     "ifd_tr_gn_fwd_gstat": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, i32, vp, i32, f32, vp, vp, vp]),
+    "ifd_tr_conv_x3_gn": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, vp, vp, i64, vp, vp, i64,
+                                vp, vp, i32, vp]),
+    "ifd_tr_conv_gn": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, i64,
+                             vp]),
+    "ifd_tr_conv_wgrad_x3_gn": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp, i64, vp, i32, vp]),
+    "ifd_tr_gn_coef": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, i32, f32, vp, vp, vp, vp, i64, vp]),
+    "ifd_tr_act_apply": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
@@ -114,18 +121,26 @@ class UNetTrainer:
     which the reference has no code for): the split kernels with ONE product per MAC (f16 operands, fp32
     accumulation) for the forward, dgrad and weight-gradient convs, the same loss scale and range guard.
     Not fp32-class: reported separately, checked against the fp32 step at a stated tolerance
-    (tests/test_gpu_train.py::test_train_f16_full_vs_fp32)."""
+    (tests/test_gpu_train.py::test_train_f16_full_vs_fp32).
+
+    fuse_gn (split modes): the GroupNorm + SiLU in front of a 3x3 conv (ResBlock in_layers / out_layers,
+    the output head) is not materialised: ifd_tr_gn_coef gives per-(image, channel) coefficients A, B,
+    the forward conv applies silu(A x + B) to the raw input on load (the sampler's prologue) and the
+    weight gradient recomputes it at staging (ifd_tr_conv_wgrad_x3_gn). Shapes a kernel does not take
+    materialise the activation (ifd_tr_act_apply) and run the plain path."""
 
     SPLIT_MODES = ("3xf16", "f16")
 
     def __init__(self, cfg: UNetConfig = FULL, device="cuda", lr=5e-5, weight_decay=0.01, betas=(0.9, 0.999),
-                 eps=1e-8, max_norm=1.0, precision="fp32", x3_dgrad=True, x3_wgrad=True, x3_loss_scale_log2=20):
+                 eps=1e-8, max_norm=1.0, precision="fp32", x3_dgrad=True, x3_wgrad=True, x3_loss_scale_log2=20,
+                 fuse_gn=True):
         if precision not in ("fp32", "3xf16", "f16"):
             raise ValueError(f"precision must be 'fp32', '3xf16' or 'f16', got {precision!r}")
         self.precision = precision
         self.x3_dgrad = bool(x3_dgrad)
         self.x3_wgrad = bool(x3_wgrad)
         self.x3_loss_scale_log2 = int(x3_loss_scale_log2)
+        self.fuse_gn = bool(fuse_gn)
         self.guard_trips = 0
         self.cfg = cfg
         self.dev = torch.device(device)
@@ -220,11 +235,12 @@ class UNetTrainer:
     def _x3_active(self, transpose):
         return self._split() and (not transpose or self.x3_dgrad)
 
-    def _conv_x3(self, x, cin_x, N, H, name, bias_name, res, x1, c1, transpose):
-        """The conv on the 3xf16 split kernel, or None when its shape is not eligible (fp32 kernel then)."""
+    def _conv_x3(self, x, cin_x, N, H, name, bias_name, res, x1, c1, transpose, gn=None):
+        """The conv on the 3xf16 split kernel, or None when its shape is not eligible (fp32 kernel then).
+        gn = (A, B): x is the raw GroupNorm input, silu(A x + B) applied on load (3x3 only)."""
         w = self.p(name)
         taps = int(np.prod(w.shape[2:])) if w.dim() > 2 else 1
-        if taps not in (1, 9):
+        if taps not in (1, 9) or (gn is not None and taps != 9):
             return None
         cout, cin = w.shape[0], w.shape[1]
         pout, pin = (cout, cin) if not transpose else (cin, cout)
@@ -254,8 +270,21 @@ class UNetTrainer:
         out = self._empty(N, H, H, ppad)
         pf = lib().ifd_tr_conv_x3_part_floats(N, H, cin_pad, ppad)
         part = self._empty(max(pf, 1))
-        if not transpose and ppad == pout and pout % 128 == 0:
+        want_stats = not transpose and ppad == pout and pout % 128 == 0
+        if gn is not None:
+            if ppad != pout:
+                return None
             # forward convs also hand the following GroupNorm its statistics (granules from the epilogue)
+            gf = lib().ifd_tr_gstat_floats(N, H, pout) if want_stats else 0
+            gstat = self._empty(max(gf, 1))
+            E, cnt = _c.c_int(0), _c.c_float(0.0)
+            rc = lib().ifd_tr_conv_x3_gn(P(x), cin_x, P(x1), c1, N, H, P(wx3), P(b), cin_pad, ppad, P(gn[0]),
+                                         P(gn[1]), P(res), P(out), P(part), pf, P(self._guard),
+                                         P(gstat) if want_stats else None, gf, _c.byref(E), _c.byref(cnt),
+                                         self._nprod(), self.s)
+            if rc == 0 and E.value > 0:
+                self._gstat[out.data_ptr()] = (out, gstat, E.value, cnt.value, pout, None)
+        elif want_stats:
             gf = lib().ifd_tr_gstat_floats(N, H, pout)
             gstat = self._empty(gf)
             E, cnt = _c.c_int(0), _c.c_float(0.0)
@@ -276,11 +305,12 @@ class UNetTrainer:
             out = real
         return out
 
-    def conv(self, x, cin_x, N, H, name, bias_name=None, res=None, x1=None, c1=0, transpose=False):
+    def conv(self, x, cin_x, N, H, name, bias_name=None, res=None, x1=None, c1=0, transpose=False, gn=None):
         """NHWC conv of concat(x[cin_x], x1[c1]) with weight `name` (forward or, transposed, dgrad).
-        Output channels are padded to a multiple of 4 (zero weight rows): the 6-channel head writes 8."""
+        Output channels are padded to a multiple of 4 (zero weight rows): the 6-channel head writes 8.
+        gn = (A, B): the conv's input is silu(A x + B) of the raw x (fuse_gn), applied on load."""
         if self._x3_active(transpose):
-            out = self._conv_x3(x, cin_x, N, H, name, bias_name, res, x1, c1, transpose)
+            out = self._conv_x3(x, cin_x, N, H, name, bias_name, res, x1, c1, transpose, gn=gn)
             if out is not None:
                 return out
         buf, pout, pin, taps, bn, cin_pad, cout_pad = self._packed(name, int(transpose))
@@ -295,12 +325,18 @@ class UNetTrainer:
             b[:real].copy_(self.p(bias_name))
         pf = lib().ifd_tr_conv_part_floats(N, H, cin_pad, pout, cout_pad, bn, taps)
         part = self._empty(max(pf, 1))
+        if gn is not None:
+            chk(lib().ifd_tr_conv_gn(P(x), cin_x, P(x1), c1, N, H, P(buf), P(b), cin_pad, pout, cout_pad, bn, taps,
+                                     P(gn[0]), P(gn[1]), P(res), P(out), P(part), pf, self.s))
+            return out
         chk(lib().ifd_tr_conv(P(x), cin_x, P(x1), c1, N, H, P(buf), P(b), cin_pad, pout, cout_pad, bn, taps, P(res),
                               P(out), P(part), pf, self.s))
         return out
 
-    def wgrad(self, dy, cout, x, cin_x, N, H, name, bias_name=None, real_cin=None):
-        """grad[name] += conv weight gradient; grad[bias] += column sums of dy."""
+    def wgrad(self, dy, cout, x, cin_x, N, H, name, bias_name=None, real_cin=None, gn=None):
+        """grad[name] += conv weight gradient; grad[bias] += column sums of dy.
+        gn = (A, B): the forward conv's input was silu(A x + B) of the raw x (recomputed at staging, or
+        materialised here when the split kernel does not take the shape)."""
         w = self.p(name)
         taps = int(np.prod(w.shape[2:])) if w.dim() > 2 else 1
         P_ = N * H * H
@@ -313,17 +349,30 @@ class UNetTrainer:
         direct = real_cin == cin_x and real_cout == cout
         dw = self.g(name) if direct else self._zeros(cout * cin_x * taps)
         db = self.g(bias_name) if (bias_name and real_cout == cout) else (self._zeros(cout) if bias_name else None)
+        rc = 3
+        if gn is not None and self._split() and self.x3_wgrad and taps == 9:
+            rc = lib().ifd_tr_conv_wgrad_x3_gn(P(dy), cout, P(x), cin_x, N, H, P(gn[0]), P(gn[1]), P(dw), P(db),
+                                               P(part), need, P(colpart), colpart.numel(), P(self._guard),
+                                               self._nprod(), self.s)
+        if rc != 3:
+            chk(rc)
+        else:
+            if gn is not None:  # the split kernel does not take this shape: materialise the activation
+                x = self.act_apply(x, N, H * H, cin_x, gn)
+            self._wgrad_plain(dy, cout, x, cin_x, N, H, taps, dw, db, part, need, colpart)
+        if not direct:  # padded input (the first conv reads 16 channels, 9 real) or output (head: 8, 6 real)
+            chk(lib().ifd_tr_copy_channels(P(dw), cin_x * taps, 0, P(self.g(name)), real_cin * taps, 0, real_cin * taps,
+                                           real_cout, 1, self.s))
+        if bias_name and real_cout != cout:
+            chk(lib().ifd_tr_copy_channels(P(db), cout, 0, P(self.g(bias_name)), real_cout, 0, real_cout, 1, 1, self.s))
+
+    def _wgrad_plain(self, dy, cout, x, cin_x, N, H, taps, dw, db, part, need, colpart):
         if self._split() and self.x3_wgrad:
             chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
                                            P(colpart), colpart.numel(), P(self._guard), self._nprod(), self.s))
         else:
             chk(lib().ifd_tr_conv_wgrad(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
                                         P(colpart), colpart.numel(), self.s))
-        if not direct:  # padded input (the first conv reads 16 channels, 9 real) or output (head: 8, 6 real)
-            chk(lib().ifd_tr_copy_channels(P(dw), cin_x * taps, 0, P(self.g(name)), real_cin * taps, 0, real_cin * taps,
-                                           real_cout, 1, self.s))
-        if bias_name and real_cout != cout:
-            chk(lib().ifd_tr_copy_channels(P(db), cout, 0, P(self.g(bias_name)), real_cout, 0, real_cout, 1, 1, self.s))
 
     def gn_fwd(self, x, N, HW, C, prefix, ss=None, ss_stride=0, silu=True):
         out = self._empty(N * HW * C)
@@ -339,6 +388,30 @@ class UNetTrainer:
         chk(lib().ifd_tr_gn_fwd(P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")), P(ss),
                                 ss_stride, int(silu), P(out), P(stats), P(work), work.numel(), self.s))
         return out, stats
+
+    def _gn_fused(self):
+        return self.fuse_gn and self._split()
+
+    def gn_coef(self, x, N, HW, C, prefix, ss=None, ss_stride=0):
+        """(A, B), stats of GroupNorm + scale/shift for a consumer that applies silu(A x + B) on load."""
+        A, B = self._empty(N, C), self._empty(N, C)
+        stats = self._empty(N * 64)
+        g = self._gstat.get(x.data_ptr())
+        gam, bet = self.p(prefix + "weight"), self.p(prefix + "bias")
+        if g is not None and g[0] is x and C % 128 == 0:
+            chk(lib().ifd_tr_gn_coef(None, N, HW, C, P(gam), P(bet), P(ss), ss_stride, P(g[1]), g[4], P(g[5]), g[2],
+                                     g[3], P(stats), P(A), P(B), None, 0, self.s))
+        else:
+            nsl = (HW + 255) // 256
+            work = torch.empty(N * nsl * 64, device=self.dev, dtype=torch.float64)
+            chk(lib().ifd_tr_gn_coef(P(x), N, HW, C, P(gam), P(bet), P(ss), ss_stride, None, 0, None, 0, 0.0,
+                                     P(stats), P(A), P(B), P(work), work.numel(), self.s))
+        return (A, B), stats
+
+    def act_apply(self, x, N, HW, C, gn, silu=True):
+        out = self._empty(N * HW * C)
+        chk(lib().ifd_tr_act_apply(P(x), N, HW, C, P(gn[0]), P(gn[1]), int(silu), P(out), self.s))
+        return out
 
     def gn_bwd(self, dout, x, N, HW, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None, silu=True):
         acc = dx is not None
@@ -437,9 +510,14 @@ class UNetTrainer:
                 elif k == "attn":
                     h = self._attn_fwd(L, h, N, hr, saved)
                 elif k == "out":
-                    a, st = self.gn_fwd(h, N, hr * hr, hc, "out.0.", silu=True)
-                    saved["out"] = dict(x=h, a=a, stats=st)
-                    h = self.conv(a, hc, N, hr, "out.2.weight", "out.2.bias")
+                    if self._gn_fused():
+                        gn, st = self.gn_coef(h, N, hr * hr, hc, "out.0.")
+                        saved["out"] = dict(x=h, a=None, gn=gn, stats=st)
+                        h = self.conv(h, hc, N, hr, "out.2.weight", "out.2.bias", gn=gn)
+                    else:
+                        a, st = self.gn_fwd(h, N, hr * hr, hc, "out.0.", silu=True)
+                        saved["out"] = dict(x=h, a=a, gn=None, stats=st)
+                        h = self.conv(a, hc, N, hr, "out.2.weight", "out.2.bias")
                     hc = L["cout"]
             if section == "input":
                 hs.append(h)
@@ -450,20 +528,31 @@ class UNetTrainer:
     def _res_fwd(self, L, x, N, r, emb, saved):
         """ResBlock._forward (code/nn.py:189-212), scale-shift norm, resblock_updown."""
         p, cin, cout, k = L["prefix"], L["cin"], L["cout"], L["kind"]
-        a1, st1 = self.gn_fwd(x, N, r * r, cin, p + "in_layers.0.", silu=True)
         mode = 1 if k == "res_up" else (2 if k == "res_down" else 0)
         ro = 2 * r if mode == 1 else (r // 2 if mode == 2 else r)
-        a1r = self.resample(a1, N, r, cin, mode) if mode else a1
+        fused = self._gn_fused()
+        g1 = g2 = a1r = a2 = None
+        if fused and not mode:  # in_layers: GroupNorm + SiLU applied by conv1's prologue (and wgrad's staging)
+            g1, st1 = self.gn_coef(x, N, r * r, cin, p + "in_layers.0.")
+            h1 = self.conv(x, cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias", gn=g1)
+        else:
+            a1, st1 = self.gn_fwd(x, N, r * r, cin, p + "in_layers.0.", silu=True)
+            a1r = self.resample(a1, N, r, cin, mode) if mode else a1
+            h1 = self.conv(a1r, cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
         xr = self.resample(x, N, r, cin, mode) if mode else x
-        h1 = self.conv(a1r, cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
         E = self.linear(emb, N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True)  # [N, 2 cout]
-        a2, st2 = self.gn_fwd(h1, N, ro * ro, cout, p + "out_layers.0.", ss=E, ss_stride=2 * cout, silu=True)
         if cin != cout:
             skip = self.conv(xr, cin, N, ro, p + "skip_connection.weight", p + "skip_connection.bias")
         else:
             skip = xr
-        out = self.conv(a2, cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias", res=skip)
-        saved[p] = dict(x=x, a1r=a1r, xr=xr, h1=h1, a2=a2, E=E, st1=st1, st2=st2, mode=mode, r=r, ro=ro)
+        if fused:  # out_layers: GroupNorm + scale/shift + SiLU in conv2's prologue
+            g2, st2 = self.gn_coef(h1, N, ro * ro, cout, p + "out_layers.0.", ss=E, ss_stride=2 * cout)
+            out = self.conv(h1, cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias", res=skip, gn=g2)
+        else:
+            a2, st2 = self.gn_fwd(h1, N, ro * ro, cout, p + "out_layers.0.", ss=E, ss_stride=2 * cout, silu=True)
+            out = self.conv(a2, cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias", res=skip)
+        saved[p] = dict(x=x, a1r=a1r, g1=g1, xr=xr, h1=h1, a2=a2, g2=g2, E=E, st1=st1, st2=st2, mode=mode, r=r,
+                        ro=ro)
         return out, ro
 
     def _attn_fwd(self, L, x, N, r, saved):
@@ -502,7 +591,10 @@ class UNetTrainer:
         so = saved["out"]
         hc = so["x"].shape[-1]
         co = dout6.shape[-1]  # the head's channel count padded to 4 (zero gradient in the pad)
-        self.wgrad(dout6, co, so["a"], hc, N, H, "out.2.weight", "out.2.bias")
+        if so["gn"] is not None:
+            self.wgrad(dout6, co, so["x"], hc, N, H, "out.2.weight", "out.2.bias", gn=so["gn"])
+        else:
+            self.wgrad(dout6, co, so["a"], hc, N, H, "out.2.weight", "out.2.bias")
         da = None
         if self._x3_active(True) and co % 16:
             # the split kernel's dgrad reads 16-channel chunks: the head gradient padded with zero channels
@@ -575,14 +667,21 @@ class UNetTrainer:
         sv = saved[p]
         cin, cout, mode, r, ro = L["cin"], L["cout"], sv["mode"], sv["r"], sv["ro"]
         # h2 = conv2(a2) + b2; out = skip + h2
-        self.wgrad(dout, cout, sv["a2"], cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias")
+        if sv["g2"] is not None:
+            self.wgrad(dout, cout, sv["h1"], cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias",
+                       gn=sv["g2"])
+        else:
+            self.wgrad(dout, cout, sv["a2"], cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias")
         da2 = self.conv(dout, cout, N, ro, p + "out_layers.3.weight", transpose=True)
         dE = self._zeros(N, 2 * cout)
         dh1 = self.gn_bwd(da2, sv["h1"], N, ro * ro, cout, p + "out_layers.0.", sv["st2"], ss=sv["E"],
                           ss_stride=2 * cout, dss=dE, silu=True)
         self.linear_bwd(dE, self._tape["emb"], N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True,
                         dx=demb)
-        self.wgrad(dh1, cout, sv["a1r"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
+        if sv["g1"] is not None:
+            self.wgrad(dh1, cout, sv["x"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias", gn=sv["g1"])
+        else:
+            self.wgrad(dh1, cout, sv["a1r"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
         da1r = self.conv(dh1, cout, N, ro, p + "in_layers.2.weight", transpose=True)
         da1 = self.resample_bwd(da1r, N, r, cin, mode) if mode else da1r
         if cin != cout:

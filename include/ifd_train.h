@@ -63,6 +63,19 @@ int ifd_tr_conv_x3_gstat(const float* x0, int c0, const float* x1, int c1, int N
                          const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
                          int64_t part_floats, unsigned* guard, int taps, float* gstat, int64_t gstat_floats,
                          int* gstat_E, float* gstat_cnt, int nprod, void* stream);
+/* GroupNorm-apply prologue variants: the conv reads the RAW GroupNorm input x = concat(x0, x1) and
+ * computes silu(actA[n][c] x + actB[n][c]) per staged value (zero padding after the activation), as the
+ * sampler's convs do; actA / actB from ifd_tr_gn_coef. The normalised activation of a ResBlock's
+ * in_layers / out_layers (code/nn.py:189-212) and the output head (code/unet.py:197-200) is then never
+ * written. ifd_tr_conv_x3_gn: 3x3 only, else as ifd_tr_conv_x3_gstat (returns 3 when not eligible);
+ * ifd_tr_conv_gn: the fp32 kernel, as ifd_tr_conv. */
+int ifd_tr_conv_x3_gn(const float* x0, int c0, const float* x1, int c1, int N, int H, const void* wx3,
+                      const float* bias, int cin_pad, int cout, const float* actA, const float* actB, const float* res,
+                      float* out, float* part, int64_t part_floats, unsigned* guard, float* gstat,
+                      int64_t gstat_floats, int* gstat_E, float* gstat_cnt, int nprod, void* stream);
+int ifd_tr_conv_gn(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* wpack,
+                   const float* bias, int cin_pad, int cout, int cout_pad, int bn, int taps, const float* actA,
+                   const float* actB, const float* res, float* out, float* part, int64_t part_floats, void* stream);
 /* x[i] *= s (the loss scale of the 3xf16 backward and its removal from the gradients). */
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream);
 /* dw[cout][c0+c1][taps] += sum_pixels dy (x) shifted concat(x0, x1); db[cout] += column sums of dy. */
@@ -77,6 +90,23 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
 int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                          int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
                          int64_t colpart_floats, unsigned* guard, int nprod, void* stream);
+/* ifd_tr_conv_wgrad_x3 (3x3) of the weight whose forward ran ifd_tr_conv_x3_gn: X = silu(actA x0 + actB),
+ * recomputed at staging from the raw x0. Returns 3 (nothing launched) for shapes the split kernel does not
+ * take: the caller then materialises X (ifd_tr_act_apply) and calls ifd_tr_conv_wgrad[_x3]. */
+int ifd_tr_conv_wgrad_x3_gn(const float* dy, int cout, const float* x0, int c0, int N, int H, const float* actA,
+                            const float* actB, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
+                            int64_t colpart_floats, unsigned* guard, int nprod, void* stream);
+/* GroupNorm statistics and apply coefficients without the apply pass: stats[n][32][2] = (mean, rstd) as
+ * ifd_tr_gn_fwd's, A[n][c] = rstd gamma (1 + scale), B[n][c] = (beta - mean rstd gamma)(1 + scale) + shift
+ * (ss as ifd_tr_gn_fwd's, or NULL). From granules (gstat0 != NULL: ifd_tr_gn_fwd_gstat's contract, x unused)
+ * or one statistics pass over x (work: N * ceil(HW/256) * 64 doubles). */
+int ifd_tr_gn_coef(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
+                   int ss_stride, const float* gstat0, int C0, const float* gstat1, int E, float cnt, float* stats,
+                   float* A, float* B, double* work, int64_t work_doubles, void* stream);
+/* out = act(A[n][c] x + B[n][c]) (silu != 0: SiLU, else the affine only), the convs' prologue arithmetic:
+ * materialises a GroupNorm-applied activation when a consumer cannot apply it on load. */
+int ifd_tr_act_apply(const float* x, int N, int HW, int C, const float* A, const float* B, int silu, float* out,
+                     void* stream);
 /* GroupNorm(32, C) (+ scale/shift: ss[n][0:C] = scale, ss[n][C:2C] = shift, row stride ss_stride) (+ SiLU).
  * stats[n][32][2] = (mean, rstd) saved for the backward; work: N * ceil(HW/256) * 64 doubles. */
 int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,

@@ -203,11 +203,11 @@ def test_train_x3_head_dgrad_fallback(record):
         if decline:
             orig = tr._conv_x3
 
-            def conv_x3(x, cin_x, N, H, name, bias_name, r, x1, c1, transpose, _orig=orig):
+            def conv_x3(x, cin_x, N, H, name, bias_name, r, x1, c1, transpose, _orig=orig, **kw):
                 if name == "out.2.weight" and transpose:
                     declined.append(cin_x)
                     return None
-                return _orig(x, cin_x, N, H, name, bias_name, r, x1, c1, transpose)
+                return _orig(x, cin_x, N, H, name, bias_name, r, x1, c1, transpose, **kw)
             tr._conv_x3 = conv_x3
         torch.manual_seed(11)
         t = torch.randint(0, 1000, (2,), device=DEV)

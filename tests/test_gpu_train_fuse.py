@@ -1,0 +1,155 @@
+"""GroupNorm applied on load in the training step (UNetTrainer fuse_gn, csrc/train_ops.hip):
+ifd_tr_gn_coef's coefficients, the forward conv's prologue (ifd_tr_conv_x3_gn / ifd_tr_conv_gn) and the
+split weight gradient's staging (ifd_tr_conv_wgrad_x3_gn) against the same ops on the materialised
+activation silu(A x + B) (ifd_tr_act_apply), and the whole 3xf16 step fused vs unfused.
+
+The fused and materialised paths compute the same activation per value (fma, then SiLU through exp2 and
+rcp); the kernels may round exp / rcp at different points, so the gates are stated as tolerances:
+  * stats: bit-identical to ifd_tr_gn_fwd's (same reduction kernels);
+  * act_apply vs gn_fwd's output:          |d| <= 1e-5 max|out| (A/B form vs (x - mean) rstd gamma + beta);
+  * conv / wgrad fused vs materialised:    rel-L2 <= 1e-6, max |d| <= 1e-5 max|ref|;
+  * full 256^2 step, B = 4, fused vs not:  loss relative 1e-6, every parameter gradient rel-L2 <= 1e-5.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _coef(x, N, HW, C, ss=None, seed=0):
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    g = torch.Generator().manual_seed(seed)
+    gamma = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    nsl = (HW + 255) // 256
+    work = torch.empty(N * nsl * 64, device=DEV, dtype=torch.float64)
+    A, B = torch.empty(N, C, device=DEV), torch.empty(N, C, device=DEV)
+    st = torch.empty(N * 64, device=DEV)
+    chk(lib().ifd_tr_gn_coef(P(x), N, HW, C, P(gamma), P(beta), P(ss), 2 * C if ss is not None else 0, None, 0, None,
+                             0, 0.0, P(st), P(A), P(B), P(work), work.numel(), s))
+    out = torch.empty(N, HW, C, device=DEV)
+    st2 = torch.empty(N * 64, device=DEV)
+    chk(lib().ifd_tr_gn_fwd(P(x), N, HW, C, P(gamma), P(beta), P(ss), 2 * C if ss is not None else 0, 1, P(out),
+                            P(st2), P(work), work.numel(), s))
+    return A, B, st, out, st2
+
+
+def _apply(x, N, HW, C, A, B):
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    out = torch.empty(N, HW, C, device=DEV)
+    chk(lib().ifd_tr_act_apply(P(x), N, HW, C, P(A), P(B), 1, P(out), _lib.stream_ptr(DEV)))
+    return out
+
+
+def _close(a, b, rel=1e-6, mx=1e-5):
+    a, b = a.double(), b.double()
+    r = float((a - b).norm() / b.norm())
+    m = float((a - b).abs().max() / b.abs().max())
+    assert r <= rel and m <= mx, (r, m)
+    return r, m
+
+
+@pytest.mark.parametrize("N,H,C,with_ss", [(2, 32, 128, False), (2, 16, 256, True), (3, 8, 64, True)])
+def test_gn_coef_matches_gn_fwd(N, H, C, with_ss):
+    g = torch.Generator().manual_seed(N * H + C)
+    x = (torch.randn(N, H, H, C, generator=g) * 1.7 + 0.4).to(DEV)
+    ss = (0.2 * torch.randn(N, 2 * C, generator=g)).to(DEV) if with_ss else None
+    A, B, st, out, st2 = _coef(x, N, H * H, C, ss, seed=C)
+    a = _apply(x, N, H * H, C, A, B)
+    torch.cuda.synchronize()
+    assert torch.equal(st, st2)
+    assert float((a - out).abs().max()) <= 1e-5 * float(out.abs().max())
+
+
+@pytest.mark.parametrize("N,H,cin,cout", [(2, 32, 128, 128), (2, 16, 256, 128), (4, 8, 128, 256)])
+def test_conv_x3_gn_matches_materialised(N, H, cin, cout, record):
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    g = torch.Generator().manual_seed(7 + H)
+    x = (torch.randn(N, H, H, cin, generator=g) + 0.3).to(DEV)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(DEV)
+    b = (0.3 * torch.randn(cout, generator=g)).to(DEV)
+    A, B, _, _, _ = _coef(x, N, H * H, cin, seed=3)
+    a = _apply(x, N, H * H, cin, A, B)
+    guard = torch.zeros(4, device=DEV, dtype=torch.int32)
+    wx3 = torch.empty(cout * cin * 9, device=DEV)
+    chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, 9, cin, cout, 0, P(wx3), P(guard), s))
+    pf = lib().ifd_tr_conv_x3_part_floats(N, H, cin, cout)
+    part = torch.empty(max(pf, 1), device=DEV)
+    ref = torch.empty(N, H, H, cout, device=DEV)
+    out = torch.empty_like(ref)
+    chk(lib().ifd_tr_conv_x3_taps(P(a), cin, None, 0, N, H, P(wx3), P(b), cin, cout, None, P(ref), P(part), pf,
+                                  P(guard), 9, 3, s))
+    E, cnt = ctypes.c_int(0), ctypes.c_float(0.0)
+    rc = lib().ifd_tr_conv_x3_gn(P(x), cin, None, 0, N, H, P(wx3), P(b), cin, cout, P(A), P(B), None, P(out), P(part),
+                                 pf, P(guard), None, 0, ctypes.byref(E), ctypes.byref(cnt), 3, s)
+    chk(rc)
+    torch.cuda.synchronize()
+    assert int(guard.max()) == 0
+    r, m = _close(out, ref)
+    record(f"train_fuse/conv_x3_gn/{N}x{H}x{cin}->{cout}", rel_l2=r, max_rel=m)
+
+
+@pytest.mark.parametrize("N,H,cin,cout", [(2, 32, 128, 128), (2, 64, 64, 128), (8, 8, 256, 256), (2, 16, 128, 8)])
+def test_wgrad_x3_gn_matches_materialised(N, H, cin, cout, record):
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    g = torch.Generator().manual_seed(11 + H + cout)
+    x = (torch.randn(N, H, H, cin, generator=g) + 0.3).to(DEV)
+    dy = torch.randn(N, H, H, cout, generator=g).to(DEV)
+    A, B, _, _, _ = _coef(x, N, H * H, cin, seed=5)
+    a = _apply(x, N, H * H, cin, A, B)
+    P_ = N * H * H
+    S = ctypes.c_int()
+    need = lib().ifd_tr_wgrad_part_floats(cout, cin, 9, P_, ctypes.byref(S))
+    part = torch.empty(need, device=DEV)
+    colpart = torch.empty(((P_ + 1023) // 1024) * cout, device=DEV)
+    guard = torch.zeros(4, device=DEV, dtype=torch.int32)
+    dw0, db0 = torch.zeros(cout * cin * 9, device=DEV), torch.zeros(cout, device=DEV)
+    dw1, db1 = torch.zeros_like(dw0), torch.zeros_like(db0)
+    chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(a), cin, None, 0, N, H, 9, P(dw0), P(db0), P(part), need,
+                                   P(colpart), colpart.numel(), P(guard), 3, s))
+    chk(lib().ifd_tr_conv_wgrad_x3_gn(P(dy), cout, P(x), cin, N, H, P(A), P(B), P(dw1), P(db1), P(part), need,
+                                      P(colpart), colpart.numel(), P(guard), 3, s))
+    torch.cuda.synchronize()
+    assert int(guard.max()) == 0
+    assert torch.equal(db0, db1)
+    r, m = _close(dw1, dw0)
+    record(f"train_fuse/wgrad_x3_gn/{N}x{H}x{cin}->{cout}", rel_l2=r, max_rel=m)
+
+
+def test_train_fuse_gn_step_matches_unfused(record):
+    """Full config, B = 4: the 3xf16 step with the GroupNorm applied on load vs materialised."""
+    from test_gpu_train import _full_step
+    res = {}
+    for fuse in (False, True):
+        tr, loss = _full_step("3xf16", fuse_gn=fuse)
+        assert tr.guard_trips == 0
+        res[fuse] = (loss, tr.grad.clone(), tr.offsets)
+        del tr
+    (l0, g0, offs), (l1, g1, _) = res[False], res[True]
+    worst, wname = 0.0, None
+    for k, (o, shape) in offs.items():
+        n = int(np.prod(shape))
+        b = g0[o:o + n].double()
+        if float(b.norm()) > 0:
+            r = float((g1[o:o + n].double() - b).norm() / b.norm())
+            if r > worst:
+                worst, wname = r, k
+    record("train_fuse/step_fused_vs_unfused", rel_loss=abs(l1 - l0) / abs(l0), max_tensor_grad_rel=worst,
+           worst_tensor=wname)
+    assert abs(l1 - l0) <= 1e-6 * abs(l0)
+    assert worst <= 1e-5, (worst, wname)
