@@ -666,16 +666,21 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       _Float16* L = lds[c & 1];
       _Float16* Ln = lds[(c + 1) & 1];
       const bool nxt = c + 1 < c_end;
-      if (TAPS == 9 && grp == 1)
-        mfma_chunk(std::integral_constant<int, 5>(), std::integral_constant<int, 4>(), L, Ln, nxt, SETc);
-      else
-        mfma_chunk(std::integral_constant<int, 0>(), std::integral_constant<int, TAPS == 9 ? 5 : 1>(), L, Ln, nxt, SETc);
+      if (c < c_end) {  // (block-uniform; the dummy half of an odd count only loads)
+        if (TAPS == 9 && grp == 1)
+          mfma_chunk(std::integral_constant<int, 5>(), std::integral_constant<int, 4>(), L, Ln, nxt, SETc);
+        else
+          mfma_chunk(std::integral_constant<int, 0>(), std::integral_constant<int, TAPS == 9 ? 5 : 1>(), L, Ln, nxt,
+                     SETc);
+      }
       load(clampc(c + 3), SETc);
       __syncthreads();
     };
+    // both halves unconditionally: every backedge leaves set 1's loads older than set 0's, so the staging
+    // waits for its own set only (wgrad_ws_kernel)
     for (int64_t c = c_beg; c < c_end; c += 2) {
       iter(c, set1);
-      if (c + 1 < c_end) iter(c + 1, set0);
+      iter(c + 1, set0);
     }
   }
   if (gmax >= 65504.0f) atomicOr(guard, 1u);
@@ -705,6 +710,308 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * TAPS + tbase + lt] = acc[lt][r];
     }
   }
+}
+
+// Warp-specialised 3x3 weight gradient (3xf16 / f16): wgrad_x3_kernel<9, ..>'s arithmetic, LDS image and
+// fragment reads, with the roles split. 8 waves, two per SIMD: waves 0-3 are consumers (quadrant w:
+// 32 co x 32 ci of all 9 taps, 144 accumulator registers), waves 4-7 producers (global loads, the
+// GroupNorm prologue, the split and the LDS writes). In wgrad_x3_kernel every wave carried a share of the
+// staging inside its own MFMA stream, and the two serialised: at the 256^2 128 -> 128 layer (B = 32) the
+// kernel ran 1.95 ms while its staging alone (MFMAs ablated) took 1.19 ms and its MFMAs alone ~0.84 ms
+// (profiles/r03k/wgrad_abl*.txt). Here a consumer's instruction stream holds only fragment reads and
+// MFMAs; the producer wave on the same SIMD issues in the MFMAs' shadow.
+// One s_barrier per chunk (both roles): the consumers' fragment reads of stage c & 1 and the producers'
+// writes of stage (c + 1) & 1 are complete (lgkmcnt(0)) before it; the producers' global loads stay in
+// flight across it (chunk c + 3's, two chunks ahead of their staging).
+constexpr int WS_NTP = 256;                                  // producer threads
+#ifndef WS_PD
+#define WS_PD 3  // consumer fragment-read distance, in (k-step, tap) steps of 3 MFMAs
+#endif
+#ifndef WS_REP
+#define WS_REP 1  // development: consumers run each staged chunk's MFMAs WS_REP times (timing only)
+#endif
+#ifndef WS_PRIO
+#define WS_PRIO 0  // consumer wave priority (s_setprio)
+#endif
+#ifndef WS_ABL
+#define WS_ABL 0  // development timing ablations (garbage results): 1 producers idle after the first chunk,
+                  // 2 consumers without MFMAs, 3 no range-guard max, 4 the split without the lo part
+#endif
+#define WS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+#if WS_ABL == 2
+#define WS_MFMA(a, b, c, x, y, z) ([&]() { asm volatile("" ::"v"(a), "v"(b)); return (c); }())
+#else
+#define WS_MFMA __builtin_amdgcn_mfma_f32_32x32x16_f16
+#endif
+template <int NPROD, bool GNA>
+__global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* guard, float* colpart) {
+  constexpr int DI = WX_PX * 16 / WS_NTP;                    // dY 16-B items per producer thread (4)
+  constexpr int XI = (WX_HMAX * 16 + WS_NTP - 1) / WS_NTP;   // X halo items per producer thread (9)
+  constexpr int NTAP = 9;
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
+  f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop
+  const int cin = a.c0;
+  const int nci = (cin + 63) / 64;
+  int tile = blockIdx.x, zs = blockIdx.y;
+  if ((gridDim.y & 7) == 0) {  // the tiles of one z on one XCD (wgrad_x3_kernel)
+    const int L = blockIdx.x + blockIdx.y * gridDim.x, j = L >> 3;
+    tile = j % gridDim.x;
+    zs = (j / gridDim.x) * 8 + (L & 7);
+  }
+  const int cit = tile % nci, cot = tile / nci;
+  const int co0 = cot * 64, ci0 = cit * 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool producer = wave >= 4;
+  const int Wc = a.W < 32 ? a.W : 32, R = WX_PX / Wc;
+  const int HWc = Wc + 2, HP = (R + 2) * HWc;
+  const int lwc = __builtin_ctz(Wc);
+  const int segs = a.W / Wc, rows_per_img = a.H / R;
+  const int64_t nch = (int64_t)a.N * rows_per_img * segs;
+  const int64_t c_beg = (int64_t)zs * a.chunks_per_split;
+  const int64_t c_end = c_beg + a.chunks_per_split < nch ? c_beg + a.chunks_per_split : nch;
+  const int lpi = __builtin_ctz(rows_per_img * segs), lsg = __builtin_ctz(segs);
+  auto chunk_origin = [&](int64_t c, int& n, int& y0, int& x0) {
+    const int ci = (int)c;
+    n = ci >> lpi;
+    const int rem = ci & ((1 << lpi) - 1);
+    y0 = (rem >> lsg) * R;
+    x0 = (rem & (segs - 1)) * Wc;
+  };
+  auto clampc = [&](int64_t c) { return c < c_end ? c : c_end - 1; };
+  const bool do_cs = colpart && cit == 0;
+
+  if (producer) {
+    const int ptid = tid - 256;
+    float gmax = 0.f;
+    f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+    if (c_beg < c_end) {
+      const int cq = ptid & 15;
+      const bool co_ok = co0 + 4 * cq + 3 < a.cout, ci_ok = ci0 + 4 * cq + 3 < cin;
+      f32x4 dvs[2][DI], xvs[2][XI];
+      f32x4 gas[GNA ? 2 : 1], gbs[GNA ? 2 : 1];
+      unsigned okm[GNA ? 2 : 1];
+      int xhy[XI], xhx[XI], ld_x[XI], ld_d[DI];
+#pragma unroll
+      for (int k = 0; k < XI; ++k) {
+        const int hp = (ptid + WS_NTP * k) >> 4;
+        xhy[k] = hp < HP ? hp / HWc - 1 : -1000000;
+        xhx[k] = hp % HWc - 1;
+        ld_x[k] = hp < HP ? ((xhy[k] * a.W + xhx[k]) * cin + ci0 + 4 * cq) * 4 : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < DI; ++k) {
+        const int m = (ptid + WS_NTP * k) >> 4;
+        ld_d[k] = (((m >> lwc) * a.W + (m & (Wc - 1))) * a.cout + co0 + 4 * cq) * 4;
+      }
+      auto load = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
+        constexpr int S = decltype(SETc)::value;
+        int n, y0, x0;
+        chunk_origin(c, n, y0, x0);
+        const rsrc_t rd = mkrsrc(a.dy + (size_t)n * a.H * a.W * a.cout);
+        const rsrc_t rx = mkrsrc(a.x0 + (size_t)n * a.H * a.W * cin);
+        const int od = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * a.cout * 4);
+        const int ox = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * cin * 4);
+#pragma unroll
+        for (int k = 0; k < DI; ++k) dvs[S][k] = bld4(rd, co_ok ? ld_d[k] + od : WX_OOB, 0);
+        unsigned m = 0;
+#pragma unroll
+        for (int k = 0; k < XI; ++k) {
+          const int y = y0 + xhy[k], x = x0 + xhx[k];
+          const bool ok = ci_ok & ((unsigned)y < (unsigned)a.H) & ((unsigned)x < (unsigned)a.W);
+          xvs[S][k] = bld4(rx, ok ? ld_x[k] + ox : WX_OOB, 0);
+          m |= ok ? 1u << k : 0u;
+        }
+        if constexpr (GNA) {
+          okm[S] = m;
+          const int oc = ci_ok ? (ci0 + 4 * cq) * 4 : WX_OOB;
+          gas[S] = bld4(mkrsrc(a.actA + (size_t)n * cin), oc, 0);
+          gbs[S] = bld4(mkrsrc(a.actB + (size_t)n * cin), oc, 0);
+        }
+      };
+      auto stage = [&](_Float16* L, auto SETc) __attribute__((always_inline)) {
+        constexpr int S = decltype(SETc)::value;
+        _Float16* X = L + WX_D;
+#pragma unroll
+        for (int it = 0; it < DI + XI; ++it) {
+          const bool isd = it < DI;
+          const int k = isd ? it : it - DI;
+          f32x4 v = isd ? dvs[S][k] : xvs[S][k];
+          const int row = (ptid + WS_NTP * k) >> 4;
+          if (!isd && row >= HP) continue;
+          if constexpr (GNA) {
+            if (!isd) {  // conv_x3.hip's prologue: padding rides in the exponent (2^+inf -> rcp -> 0)
+              const float pinf = (okm[S] >> k) & 1u ? 0.f : __builtin_inff();
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const float t = fmaf(gas[S][j], v[j], gbs[S][j]);
+                v[j] = t * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(fmaf(t, -1.4426950408889634f, pinf)));
+              }
+            }
+          }
+          if (isd && do_cs) csum += v;
+          if (WS_ABL != 3)
+            asm("v_max3_f32 %0, %0, |%1|, |%2|\n\tv_max3_f32 %0, %0, |%3|, |%4|"
+                : "+v"(gmax)
+                : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+          const int o = wx_off(row, 4 * cq);
+          _Float16* base = isd ? L : X;
+          const int lo_off = isd ? WX_PX * WX_P : WX_HMAX * WX_P;
+          if (NPROD == 3 && WS_ABL == 4) {
+            typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+            typedef float f2_t __attribute__((ext_vector_type(2)));
+            const unsigned h0 = __builtin_bit_cast(unsigned, __builtin_convertvector(f2_t{v[0], v[1]}, h2_t));
+            const unsigned h1 = __builtin_bit_cast(unsigned, __builtin_convertvector(f2_t{v[2], v[3]}, h2_t));
+            *(wx_lds_u2*)(base + o) = wx_u2{h0, h1};
+            *(wx_lds_u2*)(base + lo_off + o) = wx_u2{h0, h1};
+          } else if (NPROD == 3) {
+            unsigned h0, l0, h1, l1;
+            wx_split2(v[0], v[1], h0, l0);
+            wx_split2(v[2], v[3], h1, l1);
+            *(wx_lds_u2*)(base + o) = wx_u2{h0, h1};
+            *(wx_lds_u2*)(base + lo_off + o) = wx_u2{l0, l1};
+          } else {
+            typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+            typedef float f2_t __attribute__((ext_vector_type(2)));
+            float v0 = v[0], v1 = v[1], v2 = v[2], v3 = v[3];
+            asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+            const unsigned h0 = __builtin_bit_cast(unsigned, __builtin_convertvector(f2_t{v0, v1}, h2_t));
+            const unsigned h1 = __builtin_bit_cast(unsigned, __builtin_convertvector(f2_t{v2, v3}, h2_t));
+            *(wx_lds_u2*)(base + o) = wx_u2{h0, h1};
+          }
+        }
+      };
+      const std::integral_constant<int, 0> set0;
+      const std::integral_constant<int, 1> set1;
+      load(c_beg, set0);
+      stage(lds[c_beg & 1], set0);
+      load(clampc(c_beg + 1), set1);
+      load(clampc(c_beg + 2), set0);
+      WS_BARRIER();
+      auto iter = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
+        if (WS_ABL != 1) {
+          if (c + 1 < c_end) stage(lds[(c + 1) & 1], SETc);  // (block-uniform)
+          load(clampc(c + 3), SETc);
+        }
+        WS_BARRIER();
+      };
+      // both halves unconditionally (an odd count ends with a dummy half whose barrier the consumers
+      // match): every backedge then leaves set 1's loads older than set 0's, so each staging waits for
+      // its own set only (with a conditional second half the compiler's vmcnt merge waited for both)
+      for (int64_t c = c_beg; c < c_end; c += 2) {
+        iter(c, set1);
+        iter(c + 1, set0);
+      }
+    }
+    if (gmax >= 65504.0f) atomicOr(guard, 1u);
+    // two block-wide barriers, matched by the consumers': the stages are free, then the partial sums are in
+    if (do_cs) {  // (block-uniform)
+      WS_BARRIER();
+      csred[ptid] = csum;
+      WS_BARRIER();
+      if (ptid < 16) {
+        f32x4 t = csred[ptid];
+        for (int r = 1; r < WS_NTP / 16; ++r) t += csred[ptid + 16 * r];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = co0 + 4 * ptid + j;
+          if (co < a.cout) colpart[(size_t)zs * a.cout + co] = t[j];
+        }
+      }
+    }
+    return;
+  }
+  // consumers
+  f32x16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const int h = lane >> 5, quad = wave;
+  const int wr = 32 * (quad & 1), wc = 32 * (quad >> 1);
+  if (WS_PRIO) __builtin_amdgcn_s_setprio(WS_PRIO);
+  if (c_beg < c_end) {
+    const int G = lane >> 4, q = (lane & 15) >> 2, pcol = 4 * (lane & 3);
+    const int cA = wr + 16 * (G & 1) + pcol, cB = wc + 16 * (G & 1) + pcol;
+    WS_BARRIER();  // the first stage
+    const int64_t c_pair = c_beg + ((c_end - c_beg + 1) & ~(int64_t)1);  // (the producers' even count)
+    for (int64_t c = c_beg; c < c_pair; ++c) {
+      if (c >= c_end) {  // the producers' dummy half
+        WS_BARRIER();
+        break;
+      }
+      const _Float16* L = lds[c & 1];
+      int cAl = cA, cBl = cB, ql = q, hl = h;
+      asm volatile("" : "+v"(cAl), "+v"(cBl), "+v"(ql), "+v"(hl));
+      const _Float16* pA = L + (8 * hl + ql) * WX_P + cAl;
+      const _Float16* pB = L + WX_D + ((Wc >= 16 ? 8 * hl : hl * HWc) + ql) * WX_P + cBl;
+      auto fetchA = [&](int st, wx_h8& ahi, wx_h8& alo) {
+        const _Float16* b = pA + 16 * st * WX_P;
+        const wx_h4 ah0 = wx_tr(b, 0), ah1 = wx_tr(b, 4 * WX_P);
+        ahi = wx_h8{ah0[0], ah0[1], ah0[2], ah0[3], ah1[0], ah1[1], ah1[2], ah1[3]};
+        if (NPROD == 3) {
+          const wx_h4 al0 = wx_tr(b, WX_PX * WX_P), al1 = wx_tr(b, WX_PX * WX_P + 4 * WX_P);
+          alo = wx_h8{al0[0], al0[1], al0[2], al0[3], al1[0], al1[1], al1[2], al1[3]};
+        } else {
+          alo = ahi;
+        }
+      };
+      auto fetchB = [&](int st, int t, wx_h8& bhi, wx_h8& blo) {
+        const int m0 = 16 * st;
+        const int hb = Wc >= 16 ? (m0 >> lwc) * HWc + (m0 & (Wc - 1)) : 2 * st * HWc;
+        const int r0 = hb + (t / 3) * HWc + (t % 3);
+        const _Float16* b = pB + __builtin_amdgcn_readfirstlane(r0 * WX_P);
+        const wx_h4 bh0 = wx_tr(b, 0), bh1 = wx_tr(b, 4 * WX_P);
+        bhi = wx_h8{bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
+        if (NPROD == 3) {
+          const wx_h4 bl0 = wx_tr(b, WX_HMAX * WX_P), bl1 = wx_tr(b, WX_HMAX * WX_P + 4 * WX_P);
+          blo = wx_h8{bl0[0], bl0[1], bl0[2], bl0[3], bl1[0], bl1[1], bl1[2], bl1[3]};
+        } else {
+          blo = bhi;
+        }
+      };
+      // The chunk's 36 (k-step, tap) steps in one unrolled sequence, 3 MFMAs each into acc[tap]; the B
+      // fragments WS_PD steps ahead (one consumer wave per SIMD: nothing else covers a read's latency),
+      // the next k-step's A fragments with the first read of that k-step
+      constexpr int NST = WX_PX / 16, NS = NST * NTAP, PD = WS_PD;
+      wx_h8 bh[PD + 1], bl[PD + 1], ah[2], al[2];
+      for (int rep = 0; rep < WS_REP; ++rep) {
+      fetchA(0, ah[0], al[0]);
+#pragma unroll
+      for (int i = 0; i < PD; ++i) fetchB(i / NTAP, i % NTAP, bh[i], bl[i]);
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const int st = i / NTAP, t = i % NTAP, sl = i % (PD + 1);
+        const int j = i + PD;  // the step whose fragments are read now
+        if (j < NS) {
+          if (j % NTAP == 0) fetchA(j / NTAP, ah[(j / NTAP) & 1], al[(j / NTAP) & 1]);
+          fetchB(j / NTAP, j % NTAP, bh[j % (PD + 1)], bl[j % (PD + 1)]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc[t] = WS_MFMA(ah[st & 1], bh[sl], acc[t], 0, 0, 0);
+        if (NPROD == 3) {
+          acc[t] = WS_MFMA(ah[st & 1], bl[sl], acc[t], 0, 0, 0);
+          acc[t] = WS_MFMA(al[st & 1], bh[sl], acc[t], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      }
+      WS_BARRIER();
+    }
+  }
+  if (do_cs) {  // (the producers' two column-sum barriers)
+    WS_BARRIER();
+    WS_BARRIER();
+  }
+  float* slab = a.part + (size_t)zs * a.cout * cin * NTAP;
+  const int ci = ci0 + wc + (lane & 31);
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wr + 8 * (r >> 2) + 4 * h + (r & 3);
+      if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * NTAP + t] = acc[t][r];
+    }
 }
 
 __global__ void slab_reduce_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out,
@@ -2041,7 +2348,17 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int 
   float* cp = fused_db ? colpart : nullptr;
   const bool gna = actA != nullptr;
   const dim3 g9(tiles, S), b9(WxCfg<9>::NT), b1(WxCfg<1>::NT);
-  if (taps == 9 && nprod == 3 && gna)
+  static const int ws = getenv("IFD_WGRAD_WS") ? atoi(getenv("IFD_WGRAD_WS")) : 1;
+  if (taps == 9 && ws) {
+    if (nprod == 3 && gna)
+      hipLaunchKernelGGL((wgrad_ws_kernel<3, true>), g9, dim3(512), 0, s, a, guard, cp);
+    else if (nprod == 3)
+      hipLaunchKernelGGL((wgrad_ws_kernel<3, false>), g9, dim3(512), 0, s, a, guard, cp);
+    else if (gna)
+      hipLaunchKernelGGL((wgrad_ws_kernel<1, true>), g9, dim3(512), 0, s, a, guard, cp);
+    else
+      hipLaunchKernelGGL((wgrad_ws_kernel<1, false>), g9, dim3(512), 0, s, a, guard, cp);
+  } else if (taps == 9 && nprod == 3 && gna)
     hipLaunchKernelGGL((wgrad_x3_kernel<9, 3, true>), g9, b9, 0, s, a, guard, cp);
   else if (taps == 9 && nprod == 3)
     hipLaunchKernelGGL((wgrad_x3_kernel<9, 3, false>), g9, b9, 0, s, a, guard, cp);

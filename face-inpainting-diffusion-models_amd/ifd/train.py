@@ -823,6 +823,7 @@ class BlockTrainer(UNetTrainer):
         self._gstat = {}
         self.precision, self.x3_dgrad, self.x3_loss_scale_log2, self.guard_trips = "fp32", False, 0, 0
         self.x3_wgrad = False
+        self.fuse_gn = True  # (no effect in fp32: GroupNorm on load is a split-mode path)
         self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
         self._grad_clean = False
         self._pack_cache = {}
