@@ -735,7 +735,8 @@ constexpr int WS_NTP = 256;                                  // producer threads
 #endif
 #ifndef WS_ABL
 #define WS_ABL 0  // development timing ablations (garbage results): 1 producers idle after the first chunk,
-                  // 2 consumers without MFMAs, 3 no range-guard max, 4 the split without the lo part
+                  // 2 consumers without MFMAs, 3 no range-guard max, 4 the split without the lo part, 5 no LDS
+                  // writes, 6 no split / max (raw bits written), 7 no global loads after the first chunk
 #endif
 #define WS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #if WS_ABL == 2
@@ -788,9 +789,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
     if (c_beg < c_end) {
       const int cq = ptid & 15;
       const bool co_ok = co0 + 4 * cq + 3 < a.cout, ci_ok = ci0 + 4 * cq + 3 < cin;
-      f32x4 dvs[2][DI], xvs[2][XI];
-      f32x4 gas[GNA ? 2 : 1], gbs[GNA ? 2 : 1];
-      unsigned okm[GNA ? 2 : 1];
+      f32x4 dvs[3][DI], xvs[3][XI];
+      f32x4 gas[GNA ? 3 : 1], gbs[GNA ? 3 : 1];
+      unsigned okm[GNA ? 3 : 1];
       int xhy[XI], xhx[XI], ld_x[XI], ld_d[DI];
 #pragma unroll
       for (int k = 0; k < XI; ++k) {
@@ -806,6 +807,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
       }
       auto load = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
         constexpr int S = decltype(SETc)::value;
+        if (WS_ABL == 7 && c != c_beg) return;
         int n, y0, x0;
         chunk_origin(c, n, y0, x0);
         const rsrc_t rd = mkrsrc(a.dy + (size_t)n * a.H * a.W * a.cout);
@@ -850,14 +852,20 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
             }
           }
           if (isd && do_cs) csum += v;
-          if (WS_ABL != 3)
+          if (WS_ABL != 3 && WS_ABL != 6)
             asm("v_max3_f32 %0, %0, |%1|, |%2|\n\tv_max3_f32 %0, %0, |%3|, |%4|"
                 : "+v"(gmax)
                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
           const int o = wx_off(row, 4 * cq);
           _Float16* base = isd ? L : X;
           const int lo_off = isd ? WX_PX * WX_P : WX_HMAX * WX_P;
-          if (NPROD == 3 && WS_ABL == 4) {
+          if (WS_ABL == 5) {
+            asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(o));
+          } else if (WS_ABL == 6) {
+            const wx_u2 r0 = {__builtin_bit_cast(unsigned, v[0]), __builtin_bit_cast(unsigned, v[1])};
+            *(wx_lds_u2*)(base + o) = r0;
+            *(wx_lds_u2*)(base + lo_off + o) = r0;
+          } else if (NPROD == 3 && WS_ABL == 4) {
             typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
             typedef float f2_t __attribute__((ext_vector_type(2)));
             const unsigned h0 = __builtin_bit_cast(unsigned, __builtin_convertvector(f2_t{v[0], v[1]}, h2_t));
@@ -881,26 +889,32 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
           }
         }
       };
+      // three register sets: chunk j's loads go to set j % 3, issued at the START of iteration j - 3 (into
+      // the set chunk j - 3 was staged from), so they have three chunk-times to arrive before chunk j's
+      // staging in iteration j - 1 (with two sets issued after each staging, the producers waited on
+      // them: 1.48 ms at 256^2 without global loads vs 1.88 ms with, profiles/r04b/wgrad_*.txt)
       const std::integral_constant<int, 0> set0;
       const std::integral_constant<int, 1> set1;
+      const std::integral_constant<int, 2> set2;
       load(c_beg, set0);
       stage(lds[c_beg & 1], set0);
       load(clampc(c_beg + 1), set1);
-      load(clampc(c_beg + 2), set0);
+      load(clampc(c_beg + 2), set2);
       WS_BARRIER();
-      auto iter = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
+      auto iter = [&](int64_t c, auto LSETc, auto SSETc) __attribute__((always_inline)) {
         if (WS_ABL != 1) {
-          if (c + 1 < c_end) stage(lds[(c + 1) & 1], SETc);  // (block-uniform)
-          load(clampc(c + 3), SETc);
+          load(clampc(c + 3), LSETc);
+          if (c + 1 < c_end) stage(lds[(c + 1) & 1], SSETc);  // (block-uniform)
         }
         WS_BARRIER();
       };
-      // both halves unconditionally (an odd count ends with a dummy half whose barrier the consumers
-      // match): every backedge then leaves set 1's loads older than set 0's, so each staging waits for
-      // its own set only (with a conditional second half the compiler's vmcnt merge waited for both)
-      for (int64_t c = c_beg; c < c_end; c += 2) {
-        iter(c, set1);
-        iter(c + 1, set0);
+      // all three thirds unconditionally (a count that is not a multiple of 3 ends with dummy iterations
+      // whose barriers the consumers match): every backedge leaves the sets' loads in the same age order,
+      // so each staging waits for its own set only
+      for (int64_t c = c_beg; c < c_end; c += 3) {
+        iter(c, set0, set1);
+        iter(c + 1, set1, set2);
+        iter(c + 2, set2, set0);
       }
     }
     if (gmax >= 65504.0f) atomicOr(guard, 1u);
@@ -934,12 +948,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
     const int G = lane >> 4, q = (lane & 15) >> 2, pcol = 4 * (lane & 3);
     const int cA = wr + 16 * (G & 1) + pcol, cB = wc + 16 * (G & 1) + pcol;
     WS_BARRIER();  // the first stage
-    const int64_t c_pair = c_beg + ((c_end - c_beg + 1) & ~(int64_t)1);  // (the producers' even count)
-    for (int64_t c = c_beg; c < c_pair; ++c) {
-      if (c >= c_end) {  // the producers' dummy half
-        WS_BARRIER();
-        break;
-      }
+    for (int64_t c = c_beg; c < c_end; ++c) {
       const _Float16* L = lds[c & 1];
       int cAl = cA, cBl = cB, ql = q, hl = h;
       asm volatile("" : "+v"(cAl), "+v"(cBl), "+v"(ql), "+v"(hl));
@@ -998,6 +1007,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
       }
       WS_BARRIER();
     }
+    for (int64_t d = (c_end - c_beg) % 3; d && d < 3; ++d) WS_BARRIER();  // (the producers' dummy iterations)
   }
   if (do_cs) {  // (the producers' two column-sum barriers)
     WS_BARRIER();
