@@ -136,6 +136,9 @@ bool conv_head_x3_eligible(const ConvParams& p, int taps, int xform);
 size_t conv_head_x3_pack_floats(int cin);
 bool conv_head_x3_pack(const float* w, int cout, int cin, float* dst);
 int launch_conv_head_x3(const ConvParams& p, const float* wx, hipStream_t stream);
+// the training forward's head on the same kernel (NHWC, 8 channels) and its device-side weight packing
+bool conv_head_x3_nhwc_eligible(const ConvParams& p);
+int launch_pack_head_x3(const float* w, int cout, int cin, float* dst, unsigned* guard, hipStream_t stream);
 
 // Shared elementwise step math, also used by the standalone step kernels (sampler.hip).
 __device__ __forceinline__ float ddim_step_value(const StepCoeffs& s, float img, float eps, float noise,

@@ -356,6 +356,10 @@ __global__ __launch_bounds__(256, 2) void conv_head_x3_kernel(ConvParams p, cons
       if (p.epi == EPI_NCHW) {
 #pragma unroll
         for (int co = 0; co < CO; ++co) p.out[((size_t)n * CO + co) * HWp + pix] = a[co] + p.bias[co];
+      } else if (p.epi == EPI_NHWC) {  // the training forward: [N][H][W][8], the padded channels' rows zero
+        hx_f4* o = reinterpret_cast<hx_f4*>(p.out + ((size_t)n * HWp + pix) * HX_WCO);
+        o[0] = hx_f4{a[0] + p.bias[0], a[1] + p.bias[1], a[2] + p.bias[2], a[3] + p.bias[3]};
+        o[1] = hx_f4{a[4] + p.bias[4], a[5] + p.bias[5], a[6] + p.bias[6], a[7] + p.bias[7]};
       } else {
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -447,11 +451,54 @@ bool conv_head_x3_pack(const float* w, int cout, int cin, float* dst_f) {
   return ok;
 }
 
+// The training forward's head (include/ifd_train.h ifd_tr_conv_head_x3): NHWC output of 8 channels (the
+// 6 real ones and 2 zero-weight pads), bias padded to 8, GroupNorm + SiLU prologue.
+bool conv_head_x3_nhwc_eligible(const ConvParams& p) {
+  return !p.in1 && p.c1 == 0 && p.c0 % HX_CH == 0 && p.c0 >= HX_CH && p.c0 <= HX_MAXCH * HX_CH && !p.wskip &&
+         !p.res && p.epi == EPI_NHWC && p.cout == HX_WCO && p.H % HX_T == 0 && p.W % HX_T == 0 && p.Hin == p.H &&
+         p.Win == p.W;
+}
+
+// conv_head_x3_pack on the device (the training step re-packs every step): one thread per packed f16;
+// a weight whose split is out of range (|f16(w)| 2^11 > 65504) sets bit 2 of *guard.
+__global__ void pack_head_x3_kernel(const float* __restrict__ w, int cout, int cin, _Float16* __restrict__ dst,
+                                    unsigned* guard) {
+  const int64_t tot = (int64_t)(cin / HX_CH) * 9 * 2 * HX_WCO * HX_CH;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int c = (int)(i % HX_CH);
+  int64_t r = i / HX_CH;
+  const int co = (int)(r % HX_WCO);
+  r /= HX_WCO;
+  const int part = (int)(r % 2);
+  r /= 2;
+  const int tap = (int)(r % 9);
+  const int ch = (int)(r / 9);
+  const float v = co < cout ? w[((size_t)co * cin + ch * HX_CH + c) * 9 + tap] : 0.f;
+  const _Float16 hi = (_Float16)v;
+  _Float16 o;
+  if (part == 0) {
+    const float sc = (float)hi * 2048.0f;
+    if (!(fabsf(sc) <= 65504.0f)) atomicOr(guard, 2u);
+    o = (_Float16)sc;
+  } else {
+    o = (_Float16)((v - (float)hi) * 2048.0f);
+  }
+  dst[i] = o;
+}
+
+int launch_pack_head_x3(const float* w, int cout, int cin, float* dst, unsigned* guard, hipStream_t stream) {
+  const int64_t tot = (int64_t)(cin / HX_CH) * 9 * 2 * HX_WCO * HX_CH;
+  hipLaunchKernelGGL(pack_head_x3_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, w, cout, cin,
+                     reinterpret_cast<_Float16*>(dst), guard);
+  return (int)hipGetLastError();
+}
+
 int launch_conv_head_x3(const ConvParams& p, const float* wx, hipStream_t stream) {
   const int ntiles = p.N * (p.H / HX_T) * (p.W / HX_T);
   const int ncu = 2 * device_cu_count();  // two blocks per CU
   const int grid = ntiles < ncu ? ntiles : ncu;
-  if (p.cout == 6) {
+  if (p.cout == 6 || p.cout == HX_WCO) {  // (CO only shapes the NCHW / sampler epilogues)
     static bool attr_set[kMaxDevices] = {};
     hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_head_x3_kernel<6>), (int)HX_LDS);
     if (e != hipSuccess) return (int)e;

@@ -2082,6 +2082,33 @@ int ifd_tr_conv_gn(const float* x0, int c0, const float* x1, int c1, int N, int 
   return e;
 }
 
+int64_t ifd_tr_head_x3_pack_floats(int cin) { return (int64_t)conv_head_x3_pack_floats(cin); }
+
+int ifd_tr_conv_head_x3(const float* x, int cin, int N, int H, const float* w, int cout, float* wpack,
+                        const float* bias8, const float* actA, const float* actB, float* out, unsigned* guard,
+                        void* stream) {
+  ConvParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.in0 = x; p.c0 = cin;
+  p.N = N; p.Hin = p.Win = p.H = p.W = H;
+  p.act = ACT_AFFINE_SILU; p.actA = actA; p.actB = actB;
+  p.bias = bias8;
+  p.cin_pad = cin; p.cout = 8; p.cout_pad = 8;
+  p.out = out;
+  p.epi = EPI_NHWC;
+  p.guard = guard;
+  if (!x || !w || !wpack || !bias8 || !actA || !actB || !out || !guard || cout < 1 || cout > 8 ||
+      !conv_head_x3_nhwc_eligible(p)) {
+    set_error("ifd_tr_conv_head_x3: shape not eligible (cin % 32 == 0, cin <= 128, H % 16 == 0, cout <= 8)");
+    return 3;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  int e = launch_pack_head_x3(w, cout, cin, wpack, guard, s);
+  if (!e) e = launch_conv_head_x3(p, wpack, s);
+  if (e) set_error(std::string("ifd_tr_conv_head_x3: ") + hipGetErrorString((hipError_t)e));
+  return e;
+}
+
 int ifd_tr_pack_conv_x3(const float* w, int cout, int cin, int taps, int cin_pad16, int cout_pad, int transpose,
                         void* wx3, unsigned* guard, void* stream) {
   if (!w || !wx3 || !guard || (taps != 9 && taps != 1) || cin_pad16 % (taps == 1 ? 32 : 16) || cout_pad % 64) {

@@ -49,6 +49,8 @@ TRAIN_EXPORTS = {
     "ifd_tr_conv_wgrad_x3_gn": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp, i64, vp, i32, vp]),
     "ifd_tr_gn_coef": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, i32, f32, vp, vp, vp, vp, i64, vp]),
     "ifd_tr_act_apply": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp]),
+    "ifd_tr_head_x3_pack_floats": (i64, [i32]),
+    "ifd_tr_conv_head_x3": (i32, [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
     "ifd_tr_conv": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i64, vp]),
     "ifd_tr_wgrad_part_floats": (i64, [i32, i32, i32, i64, _c.POINTER(i32)]),
@@ -305,6 +307,22 @@ class UNetTrainer:
             out = real
         return out
 
+    def _head_x3(self, x, cin, N, H, gn):
+        """The output head's conv (GroupNorm + SiLU on load) on the split head kernel, NHWC [N,H,H,8];
+        shapes it does not take run conv() (the fp32 kernel with the same prologue)."""
+        w = self.p("out.2.weight")
+        if self.precision == "3xf16" and w.shape[0] <= 8:
+            wp = self._empty(max(lib().ifd_tr_head_x3_pack_floats(cin), 1))
+            b8 = self._zeros(8)
+            b8[:w.shape[0]].copy_(self.p("out.2.bias"))
+            out = self._empty(N, H, H, 8)
+            rc = lib().ifd_tr_conv_head_x3(P(x), cin, N, H, P(w), w.shape[0], P(wp), P(b8), P(gn[0]), P(gn[1]), P(out),
+                                           P(self._guard), self.s)
+            if rc != 3:
+                chk(rc)
+                return out
+        return self.conv(x, cin, N, H, "out.2.weight", "out.2.bias", gn=gn)
+
     def conv(self, x, cin_x, N, H, name, bias_name=None, res=None, x1=None, c1=0, transpose=False, gn=None):
         """NHWC conv of concat(x[cin_x], x1[c1]) with weight `name` (forward or, transposed, dgrad).
         Output channels are padded to a multiple of 4 (zero weight rows): the 6-channel head writes 8.
@@ -513,7 +531,7 @@ class UNetTrainer:
                     if self._gn_fused():
                         gn, st = self.gn_coef(h, N, hr * hr, hc, "out.0.")
                         saved["out"] = dict(x=h, a=None, gn=gn, stats=st)
-                        h = self.conv(h, hc, N, hr, "out.2.weight", "out.2.bias", gn=gn)
+                        h = self._head_x3(h, hc, N, hr, gn)
                     else:
                         a, st = self.gn_fwd(h, N, hr * hr, hc, "out.0.", silu=True)
                         saved["out"] = dict(x=h, a=a, gn=None, stats=st)

@@ -76,6 +76,15 @@ int ifd_tr_conv_x3_gn(const float* x0, int c0, const float* x1, int c1, int N, i
 int ifd_tr_conv_gn(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* wpack,
                    const float* bias, int cin_pad, int cout, int cout_pad, int bn, int taps, const float* actA,
                    const float* actB, const float* res, float* out, float* part, int64_t part_floats, void* stream);
+/* The output head's forward (code/unet.py:197-200: GroupNorm + SiLU + conv 3x3 -> 6) on the sampler's split
+ * head kernel (conv_head.hip): out[N,H,H,8] = conv(silu(actA x + actB)) + bias8 with channels 6, 7 zero
+ * (bias8 padded with zeros); w = the raw [cout][cin][3][3] weight (cout <= 8), re-packed on the device
+ * into wpack (ifd_tr_head_x3_pack_floats(cin) floats; |w| >= 32 sets bit 2 of *guard). cin % 32 == 0,
+ * cin <= 128, H % 16 == 0; returns 3 (nothing launched) otherwise. */
+int64_t ifd_tr_head_x3_pack_floats(int cin);
+int ifd_tr_conv_head_x3(const float* x, int cin, int N, int H, const float* w, int cout, float* wpack,
+                        const float* bias8, const float* actA, const float* actB, float* out, unsigned* guard,
+                        void* stream);
 /* x[i] *= s (the loss scale of the 3xf16 backward and its removal from the gradients). */
 int ifd_tr_scale(float* x, int64_t n, float s, void* stream);
 /* dw[cout][c0+c1][taps] += sum_pixels dy (x) shifted concat(x0, x1); db[cout] += column sums of dy. */

@@ -153,3 +153,37 @@ def test_train_fuse_gn_step_matches_unfused(record):
            worst_tensor=wname)
     assert abs(l1 - l0) <= 1e-6 * abs(l0)
     assert worst <= 1e-5, (worst, wname)
+
+
+@pytest.mark.parametrize("N,H,cin", [(2, 32, 128), (3, 16, 64)])
+def test_head_x3_matches_fp32(N, H, cin, record):
+    """ifd_tr_conv_head_x3 (the split head kernel, NHWC 8 channels) vs the fp32 conv kernel with the same
+    GroupNorm + SiLU prologue (ifd_tr_conv_gn): rel-L2 <= 1e-6, padded channels exactly zero."""
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    g = torch.Generator().manual_seed(N + H + cin)
+    x = (torch.randn(N, H, H, cin, generator=g) + 0.3).to(DEV)
+    w = (torch.randn(6, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(DEV)
+    b = (0.1 * torch.randn(6, generator=g)).to(DEV)
+    A, B, _, _, _ = _coef(x, N, H * H, cin, seed=9)
+    b8 = torch.zeros(8, device=DEV)
+    b8[:6] = b
+    guard = torch.zeros(4, device=DEV, dtype=torch.int32)
+    wp = torch.empty(lib().ifd_tr_head_x3_pack_floats(cin), device=DEV)
+    out = torch.full((N, H, H, 8), float("nan"), device=DEV)
+    chk(lib().ifd_tr_conv_head_x3(P(x), cin, N, H, P(w), 6, P(wp), P(b8), P(A), P(B), P(out), P(guard), s))
+    # the fp32 reference: weights packed for the fp32 kernel (cout padded to 8, bn 32)
+    wpk = torch.empty(32 * cin * 9, device=DEV)
+    chk(lib().ifd_tr_pack_conv(P(w), 6, cin, 9, 32, cin, 32, 0, P(wpk), s))
+    ref = torch.empty(N, H, H, 8, device=DEV)
+    pf = lib().ifd_tr_conv_part_floats(N, H, cin, 8, 32, 32, 9)
+    part = torch.empty(max(pf, 1), device=DEV)
+    chk(lib().ifd_tr_conv_gn(P(x), cin, None, 0, N, H, P(wpk), P(b8), cin, 8, 32, 32, 9, P(A), P(B), None, P(ref),
+                             P(part), pf, s))
+    torch.cuda.synchronize()
+    assert int(guard.max()) == 0
+    assert float(out[..., 6:].abs().max()) == 0.0
+    r, m = _close(out[..., :6], ref[..., :6])
+    record(f"train_fuse/head_x3/{N}x{H}x{cin}", rel_l2=r, max_rel=m)
