@@ -8,7 +8,8 @@ Inputs (rocprofv3 --pmc CSVs, one pass each, same bench command):
 Corrections (MI355X_MICROARCH.md §HBM, re-measured by pmc_cal): HBM bytes = FETCH_SIZE x f_read +
 WRITE_SIZE x f_write with f = true bytes / counter bytes of the calibration kernels.
 MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 4 SIMDs x 256 CUs)
-(GRBM_GUI_ACTIVE is summed over the 8 XCDs; MFMA busy cycles over every SIMD).
+(GRBM_GUI_ACTIVE is summed over the 8 XCDs; MFMA busy cycles over every SIMD). Effective clock per dispatch
+= GRBM_GUI_ACTIVE / 8 / dispatch duration (MI355X_MICROARCH.md, DVFS give-back), median over launches.
 usage: python tools/pmc_summary.py gpurun_out TAG [lib_sha16] > summary.json
 """
 import csv
@@ -37,6 +38,11 @@ def per_kernel(rs):
     acc = defaultdict(lambda: defaultdict(list))
     for r in rs:
         acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            # effective shader clock of the dispatch: GUI-active cycles (summed over the 8 XCDs) / 8 / duration
+            ns = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+            if ns > 0:
+                acc[short(r["Kernel_Name"])]["_clock_ghz"].append(float(r["Counter_Value"]) / 8 / ns)
     return acc
 
 
@@ -74,5 +80,10 @@ for k in sorted(set(fetch) | set(mf)):
             d["mfma_mops_f16_per_launch"] = sum(mf[k]["SQ_INSTS_VALU_MFMA_MOPS_F16"]) / len(mf[k]["SQ_INSTS_VALU_MFMA_MOPS_F16"])
         d["sq_busy_frac"] = sum(mf[k]["SQ_BUSY_CYCLES"]) / (gui / 8 * CUS) if mf[k].get("SQ_BUSY_CYCLES") else None
         d["gui_active_cycles_per_launch"] = gui / 8 / len(mf[k]["GRBM_GUI_ACTIVE"])
+        if mf[k].get("_clock_ghz"):
+            ck = sorted(mf[k]["_clock_ghz"])
+            d["eff_clock_ghz_median"] = ck[len(ck) // 2]
+            # MFMA busy x clock / 2.4 GHz nominal = the fraction of the nominal dense peak the launch reached
+            d["busy_x_clock_over_nominal"] = d["mfma_busy_frac"] * ck[len(ck) // 2] / 2.4
     out["kernels"][k] = d
 print(json.dumps(out, indent=1))
