@@ -1070,7 +1070,18 @@ __global__ void colsum_final_kernel(const float* __restrict__ part, int S, int C
 //   stats[n][g] = (mean, rstd), rstd = 1/sqrt(var + 1e-5), biased var, accumulated in float64;
 //   out = act((x - mean) * rstd * gamma + beta) [ * (1 + scale) + shift ]
 // ss (optional): [N][ss_stride], scale at [0, C), shift at [C, 2C) (the emb projection's chunk order).
-constexpr int GN_SL = 256;  // pixels per partial block
+constexpr int GN_SL = 256;  // pixels per partial block (at most; gn_nsl)
+// Slices per image of the GroupNorm passes: 256-pixel slices, halved (down to 16 pixels, not below the
+// block's pixel-row count 1024 / C) while the grid has fewer than 1024 blocks — at 16x16 and B = 32 one
+// slice per image gave 32 blocks for the whole chip (the 16^2 backward passes ran ~57 us for 17 MB).
+// The kernels take their slice length from the grid: sl = ceil(HW / gridDim.x).
+static int gn_nsl(int HW, int N, int C) {
+  int sl = GN_SL;
+  const int R = C >= 4 ? 1024 / C : 256;
+  while (sl > 16 && sl / 2 >= R && (int64_t)((HW + sl - 1) / sl) * N < 1024) sl /= 2;
+  return (HW + sl - 1) / sl;
+}
+__device__ __forceinline__ int gn_sl(int HW) { return (HW + (int)gridDim.x - 1) / (int)gridDim.x; }
 // grid (slices, N), 256 threads. Thread = (row r, channel quad q): Q = C/4 quads side by side and
 // R = 256/Q rows striding the slice's pixels, so each 16-B load belongs to a wave that covers whole
 // pixel rows. Per-thread float64 sums are combined over the rows in LDS in a fixed order.
@@ -1078,7 +1089,7 @@ __global__ __launch_bounds__(256) void gn_stat_partial_kernel(const float* __res
                                                               double* __restrict__ part) {
   __shared__ double s1[1024], s2[1024];  // [row][C] (R * C <= 1024), then per channel in row 0
   const int n = blockIdx.y;
-  const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, HW);
+  const int sl = gn_sl(HW), p0 = blockIdx.x * sl, p1 = min(p0 + sl, HW);
   const int Q = C >> 2, R = 256 / Q;
   const int q = threadIdx.x % Q, r = threadIdx.x / Q;
   if (r < R) {
@@ -1220,7 +1231,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
                                                        const float* __restrict__ beta, const float* __restrict__ ss,
                                                        int ss_stride, int act_silu, float* __restrict__ out) {
   const int n = blockIdx.y;
-  const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, HW);
+  const int sl = gn_sl(HW), p0 = blockIdx.x * sl, p1 = min(p0 + sl, HW);
   const int Q = C >> 2, R = 256 / Q;
   const int q = threadIdx.x % Q, r = threadIdx.x / Q;
   if (r >= R) return;
@@ -1268,7 +1279,7 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnBwdArgs a, float*
   // part [N][nsl][C][3]
   __shared__ float red[3][1024];  // [row][C] (R * C <= 1024), then per channel in row 0
   const int n = blockIdx.y, C = a.C;
-  const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, a.HW);
+  const int sl = gn_sl(a.HW), p0 = blockIdx.x * sl, p1 = min(p0 + sl, a.HW);
   const int Q = C >> 2, R = 256 / Q;
   const int q = threadIdx.x % Q, r = threadIdx.x / Q;
   if (r < R) {
@@ -1378,7 +1389,7 @@ __global__ void gn_bwd_param_kernel(GnBwdArgs a, const float* __restrict__ nc, f
 __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(GnBwdArgs a, const float* __restrict__ red,
                                                         float* __restrict__ dx, int accumulate) {
   const int n = blockIdx.y, C = a.C;
-  const int p0 = blockIdx.x * GN_SL, p1 = min(p0 + GN_SL, a.HW);
+  const int sl = gn_sl(a.HW), p0 = blockIdx.x * sl, p1 = min(p0 + sl, a.HW);
   const int Q = C >> 2, R = 256 / Q;
   const int q = threadIdx.x % Q, r = threadIdx.x / Q;
   if (r >= R) return;
@@ -2428,9 +2439,9 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int 
 int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
                   int ss_stride, int act_silu, float* out, float* stats, double* work, int64_t work_doubles,
                   void* stream) {
-  const int nsl = (HW + GN_SL - 1) / GN_SL;
+  const int nsl = gn_nsl(HW, N, C);
   if (C % 32 || C > 1024 || (int64_t)N * nsl * 64 > work_doubles) {
-    set_error("ifd_tr_gn_fwd: C must be a multiple of 32 (<= 1024), work >= N * ceil(HW/256) * 64 doubles");
+    set_error("ifd_tr_gn_fwd: C must be a multiple of 32 (<= 1024), work >= N * ifd_tr_gn_slices(HW, N, C) * 64 doubles");
     return 2;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -2452,11 +2463,13 @@ int ifd_tr_gn_fwd_gstat(const float* x, int N, int HW, int C, const float* gamma
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gn_granule_final_kernel, dim3(N * 32), dim3(64), 0, s, gstat0, C0, gstat1, E, cnt, C, stats,
                      GnCoef{});
-  const int nsl = (HW + GN_SL - 1) / GN_SL;
+  const int nsl = gn_nsl(HW, N, C);
   hipLaunchKernelGGL(gn_apply_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, stats, gamma, beta, ss, ss_stride,
                      act_silu, out);
   return TR_LAST();
 }
+
+int64_t ifd_tr_gn_slices(int HW, int N, int C) { return gn_nsl(HW, N, C); }
 
 int ifd_tr_gn_coef(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
                    int ss_stride, const float* gstat0, int C0, const float* gstat1, int E, float cnt, float* stats,
@@ -2475,9 +2488,9 @@ int ifd_tr_gn_coef(const float* x, int N, int HW, int C, const float* gamma, con
     hipLaunchKernelGGL(gn_granule_final_kernel, dim3(N * 32), dim3(64), 0, s, gstat0, C0, gstat1, E, cnt, C, stats, k);
     return TR_LAST();
   }
-  const int nsl = (HW + GN_SL - 1) / GN_SL;
+  const int nsl = gn_nsl(HW, N, C);
   if (!x || (int64_t)N * nsl * 64 > work_doubles) {
-    set_error("ifd_tr_gn_coef: work >= N * ceil(HW/256) * 64 doubles");
+    set_error("ifd_tr_gn_coef: work >= N * ifd_tr_gn_slices(HW, N, C) * 64 doubles");
     return 2;
   }
   hipLaunchKernelGGL(gn_stat_partial_kernel, dim3(nsl, N), dim3(256), 0, s, x, HW, C, work);
@@ -2497,7 +2510,7 @@ int ifd_tr_act_apply(const float* x, int N, int HW, int C, const float* A, const
 int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
                   const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
                   float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream) {
-  const int nsl = (HW + GN_SL - 1) / GN_SL;
+  const int nsl = gn_nsl(HW, N, C);
   const int64_t need = (int64_t)N * nsl * C * 3 + (int64_t)N * C * 3 + (int64_t)N * 64;
   if (C % 32 || C > 1024 || need > work_floats) {
     set_error("ifd_tr_gn_bwd: C must be a multiple of 32 (<= 1024); work too small");

@@ -47,6 +47,7 @@ TRAIN_EXPORTS = {
     "ifd_tr_conv_gn": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, i64,
                              vp]),
     "ifd_tr_conv_wgrad_x3_gn": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp, i64, vp, i32, vp]),
+    "ifd_tr_gn_slices": (i64, [i32, i32, i32]),
     "ifd_tr_gn_coef": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, i32, f32, vp, vp, vp, vp, i64, vp]),
     "ifd_tr_act_apply": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp]),
     "ifd_tr_head_x3_pack_floats": (i64, [i32]),
@@ -401,7 +402,7 @@ class UNetTrainer:
                                           P(ss), ss_stride, int(silu), P(g[1]), g[4], P(g[5]), g[2], g[3], P(out),
                                           P(stats), self.s))
             return out, stats
-        nsl = (HW + 255) // 256
+        nsl = lib().ifd_tr_gn_slices(HW, N, C)
         work = torch.empty(N * nsl * 64, device=self.dev, dtype=torch.float64)
         chk(lib().ifd_tr_gn_fwd(P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")), P(ss),
                                 ss_stride, int(silu), P(out), P(stats), P(work), work.numel(), self.s))
@@ -420,7 +421,7 @@ class UNetTrainer:
             chk(lib().ifd_tr_gn_coef(None, N, HW, C, P(gam), P(bet), P(ss), ss_stride, P(g[1]), g[4], P(g[5]), g[2],
                                      g[3], P(stats), P(A), P(B), None, 0, self.s))
         else:
-            nsl = (HW + 255) // 256
+            nsl = lib().ifd_tr_gn_slices(HW, N, C)
             work = torch.empty(N * nsl * 64, device=self.dev, dtype=torch.float64)
             chk(lib().ifd_tr_gn_coef(P(x), N, HW, C, P(gam), P(bet), P(ss), ss_stride, None, 0, None, 0, 0.0,
                                      P(stats), P(A), P(B), P(work), work.numel(), self.s))
@@ -437,7 +438,7 @@ class UNetTrainer:
             dx = self._empty(N * HW * C)
         else:
             self._dirty(dx)
-        nsl = (HW + 255) // 256
+        nsl = lib().ifd_tr_gn_slices(HW, N, C)
         work = self._empty(N * nsl * C * 3 + N * C * 3 + N * 64)
         chk(lib().ifd_tr_gn_bwd(P(dout), P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")),
                                 P(ss), ss_stride, int(silu), P(stats), P(dx), int(acc), P(self.g(prefix + "weight")),

@@ -108,7 +108,7 @@ int ifd_tr_conv_wgrad_x3_gn(const float* dy, int cout, const float* x0, int c0, 
 /* GroupNorm statistics and apply coefficients without the apply pass: stats[n][32][2] = (mean, rstd) as
  * ifd_tr_gn_fwd's, A[n][c] = rstd gamma (1 + scale), B[n][c] = (beta - mean rstd gamma)(1 + scale) + shift
  * (ss as ifd_tr_gn_fwd's, or NULL). From granules (gstat0 != NULL: ifd_tr_gn_fwd_gstat's contract, x unused)
- * or one statistics pass over x (work: N * ceil(HW/256) * 64 doubles). */
+ * or one statistics pass over x (work: N * ifd_tr_gn_slices(HW, N, C) * 64 doubles). */
 int ifd_tr_gn_coef(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
                    int ss_stride, const float* gstat0, int C0, const float* gstat1, int E, float cnt, float* stats,
                    float* A, float* B, double* work, int64_t work_doubles, void* stream);
@@ -116,8 +116,11 @@ int ifd_tr_gn_coef(const float* x, int N, int HW, int C, const float* gamma, con
  * materialises a GroupNorm-applied activation when a consumer cannot apply it on load. */
 int ifd_tr_act_apply(const float* x, int N, int HW, int C, const float* A, const float* B, int silu, float* out,
                      void* stream);
+/* Pixel slices per image of the GroupNorm passes (ifd_tr_gn_fwd / _coef / _bwd work sizes use it): 256-pixel
+ * slices, smaller on small maps so that the grid keeps >= 1024 blocks. */
+int64_t ifd_tr_gn_slices(int HW, int N, int C);
 /* GroupNorm(32, C) (+ scale/shift: ss[n][0:C] = scale, ss[n][C:2C] = shift, row stride ss_stride) (+ SiLU).
- * stats[n][32][2] = (mean, rstd) saved for the backward; work: N * ceil(HW/256) * 64 doubles. */
+ * stats[n][32][2] = (mean, rstd) saved for the backward; work: N * ifd_tr_gn_slices(HW, N, C) * 64 doubles. */
 int ifd_tr_gn_fwd(const float* x, int N, int HW, int C, const float* gamma, const float* beta, const float* ss,
                   int ss_stride, int act_silu, float* out, float* stats, double* work, int64_t work_doubles,
                   void* stream);
@@ -128,7 +131,7 @@ int ifd_tr_gn_fwd_gstat(const float* x, int N, int HW, int C, const float* gamma
                         int ss_stride, int act_silu, const float* gstat0, int C0, const float* gstat1, int E,
                         float cnt, float* out, float* stats, void* stream);
 /* its backward: dx (= or +=), dgamma/dbeta +=, dss (d scale, d shift) +=.
- * work: N*ceil(HW/256)*C*3 + N*C*3 + N*64 floats. */
+ * work: N * ifd_tr_gn_slices(HW, N, C) * C * 3 + N*C*3 + N*64 floats. */
 int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
                   const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
                   float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream);

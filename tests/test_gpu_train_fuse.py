@@ -28,7 +28,7 @@ def _coef(x, N, HW, C, ss=None, seed=0):
     g = torch.Generator().manual_seed(seed)
     gamma = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
     beta = (0.1 * torch.randn(C, generator=g)).to(DEV)
-    nsl = (HW + 255) // 256
+    nsl = lib().ifd_tr_gn_slices(HW, N, C)
     work = torch.empty(N * nsl * 64, device=DEV, dtype=torch.float64)
     A, B = torch.empty(N, C, device=DEV), torch.empty(N, C, device=DEV)
     st = torch.empty(N * 64, device=DEV)

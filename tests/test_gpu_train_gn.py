@@ -60,7 +60,7 @@ def test_gn_fwd_bwd(N, HW, C, use_ss, silu, acc):
     f = lambda t: None if t is None else t.detach().float().contiguous().to(DEV)  # noqa: E731
     xd, gd, bd, sd, dd = f(x), f(gamma), f(beta), f(ss), f(dout)
     s = _lib.stream_ptr(DEV)
-    nsl = (HW + 255) // 256
+    nsl = lib().ifd_tr_gn_slices(HW, N, C)
     out = torch.empty(N, HW, C, device=DEV)
     stats = torch.empty(N * 64, device=DEV)
     work = torch.empty(N * nsl * 64, device=DEV, dtype=torch.float64)

@@ -59,7 +59,7 @@ def _gn(x, N, HW, C, src):
     out = torch.empty(N, HW, C, device=DEV)
     stats = torch.empty(N * 64, device=DEV)
     if src is None:
-        nsl = (HW + 255) // 256
+        nsl = lib().ifd_tr_gn_slices(HW, N, C)
         work = torch.empty(N * nsl * 64, device=DEV, dtype=torch.float64)
         chk(lib().ifd_tr_gn_fwd(P(x), N, HW, C, P(gamma), P(beta), None, 0, 1, P(out), P(stats), P(work), work.numel(),
                                 s))

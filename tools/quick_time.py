@@ -14,7 +14,7 @@ t = torch.full((B,), 500, device=dev)
 with torch.no_grad():
     for _ in range(2): y = m(x, t, masked_image=x, mask=mk)
     torch.cuda.synchronize()
-    n = 5
+    n = int(os.environ.get("QT_N", "5"))
     t0 = time.time()
     for _ in range(n): y = m(x, t, masked_image=x, mask=mk)
     torch.cuda.synchronize()
