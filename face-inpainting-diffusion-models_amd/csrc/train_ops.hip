@@ -399,6 +399,8 @@ struct WxCfg {
 // product only; no lo planes are staged or read).
 // GNA: the X operand is the GroupNorm-applied, SiLU-activated raw input (WgArgs::actA / actB), computed
 // per staged value exactly as conv_x3.hip's producers compute it for the forward conv.
+// Launched for the 1x1 weight gradients; the 3x3 ones run wgrad_ws_kernel (below), whose consumer waves
+// carry no staging (this kernel's TAPS = 9 form measured 1.98 vs 1.79 ms, profiles/r04b/wgrad_exp).
 template <int TAPS, int NPROD, bool GNA>
 __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
   using Cf = WxCfg<TAPS>;
@@ -2396,8 +2398,10 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int 
   float* cp = fused_db ? colpart : nullptr;
   const bool gna = actA != nullptr;
   const dim3 g9(tiles, S), b9(WxCfg<9>::NT), b1(WxCfg<1>::NT);
-  static const int ws = getenv("IFD_WGRAD_WS") ? atoi(getenv("IFD_WGRAD_WS")) : 1;
-  if (taps == 9 && ws) {
+  // 3x3: the warp-specialised kernel (wgrad_x3_kernel<9, ..> measured 1.98 vs 1.79 ms at 256^2 128 -> 128,
+  // profiles/r04b/wgrad_exp); 1x1: wgrad_x3_kernel<1, ..>
+  (void)b9;
+  if (taps == 9) {
     if (nprod == 3 && gna)
       hipLaunchKernelGGL((wgrad_ws_kernel<3, true>), g9, dim3(512), 0, s, a, guard, cp);
     else if (nprod == 3)
@@ -2406,15 +2410,7 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int 
       hipLaunchKernelGGL((wgrad_ws_kernel<1, true>), g9, dim3(512), 0, s, a, guard, cp);
     else
       hipLaunchKernelGGL((wgrad_ws_kernel<1, false>), g9, dim3(512), 0, s, a, guard, cp);
-  } else if (taps == 9 && nprod == 3 && gna)
-    hipLaunchKernelGGL((wgrad_x3_kernel<9, 3, true>), g9, b9, 0, s, a, guard, cp);
-  else if (taps == 9 && nprod == 3)
-    hipLaunchKernelGGL((wgrad_x3_kernel<9, 3, false>), g9, b9, 0, s, a, guard, cp);
-  else if (taps == 9 && gna)
-    hipLaunchKernelGGL((wgrad_x3_kernel<9, 1, true>), g9, b9, 0, s, a, guard, cp);
-  else if (taps == 9)
-    hipLaunchKernelGGL((wgrad_x3_kernel<9, 1, false>), g9, b9, 0, s, a, guard, cp);
-  else if (nprod == 3)
+  } else if (nprod == 3)
     hipLaunchKernelGGL((wgrad_x3_kernel<1, 3, false>), g9, b1, 0, s, a, guard, cp);
   else
     hipLaunchKernelGGL((wgrad_x3_kernel<1, 1, false>), g9, b1, 0, s, a, guard, cp);
