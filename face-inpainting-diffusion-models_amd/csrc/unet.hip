@@ -881,9 +881,9 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   } else if (x3_geo) {  // not split-eligible after all: the fp32 kernels' own geometry
     conv_geometry(p, H, H, N, cw.bn, cw.cin_pad / 8);
   }
-  // the output head (cout 6): fp32 VALU kernel, or in the 3xf16 mode the split-MFMA head
+  // the output head (cout 6): fp32 VALU kernel, or in the split modes (3xf16, f16) the split-MFMA head
   const bool use_head = !use_x3 && cw.head_off && conv_head_eligible(p, cw.taps, xf);
-  const bool use_head_x3 = use_head && prec_ == IFD_PREC_3XF16 && cw.head_x3_ok && !(opt_x3_off_ & 32) &&
+  const bool use_head_x3 = use_head && split_ && cw.head_x3_ok && !(opt_x3_off_ & 32) &&
                            conv_head_x3_eligible(p, cw.taps, xf);
   const bool use_stream = !use_head && (use_x3 || (stream_mode != 0 && conv_stream_eligible(p, cw.taps, xf, cw.bn)));
   // fused GroupNorm statistics of the output (single-image tiles, no split-K; not mode 1)
