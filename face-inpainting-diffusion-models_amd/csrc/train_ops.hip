@@ -408,7 +408,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
   constexpr int HALO = TAPS == 9 ? 1 : 0;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
   f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop (its last barrier)
-  const int cin = a.c0;
+  const int cin = a.c0 + a.c1;  // (X = concat(x0[c0], x1[c1]): a 64-channel tile never straddles them)
   const int nci = (cin + 63) / 64;
   // (channel tile, pixel split z) of this block. Workgroups go to the 8 XCDs round-robin in launch order;
   // when the split count allows, the tiles of one z (the same dY rows and X halos) are put on one XCD so
@@ -421,6 +421,9 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
   }
   const int cit = tile % nci, cot = tile / nci;
   const int co0 = cot * 64, ci0 = cit * 64;
+  const bool src1 = a.c1 && ci0 >= a.c0;  // the tile's X source (block-uniform), its row stride, channel base
+  const float* const xsrc = src1 ? a.x1 : a.x0;
+  const int xst = src1 ? a.c1 : a.c0, xc0 = src1 ? ci0 - a.c0 : ci0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5;
   const int quad = wave & 3, grp = Cf::NG > 1 ? wave >> 2 : 0;  // quadrant; tap group (taps 0-4 / 5-8)
@@ -454,7 +457,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       const int hp = (tid + NT * k) >> 4;
       xhy[k] = hp < HP ? hp / HWc - HALO : -1000000;  // halo row / column relative to the chunk origin
       xhx[k] = hp % HWc - HALO;
-      ld_x[k] = hp < HP ? ((xhy[k] * a.W + xhx[k]) * cin + ci0 + 4 * cq) * 4 : 0;  // bytes from the chunk origin
+      ld_x[k] = hp < HP ? ((xhy[k] * a.W + xhx[k]) * xst + xc0 + 4 * cq) * 4 : 0;  // bytes from the chunk origin
     }
 #pragma unroll
     for (int k = 0; k < WX_DI; ++k) {
@@ -479,9 +482,9 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       // buffer loads from the chunk's image (SGPR descriptors, one add per load for the chunk origin);
       // a padding / out-of-tile lane reads at an offset past the descriptor's range, which returns zeros
       const rsrc_t rd = mkrsrc(a.dy + (size_t)n * a.H * a.W * a.cout);
-      const rsrc_t rx = mkrsrc(a.x0 + (size_t)n * a.H * a.W * cin);
+      const rsrc_t rx = mkrsrc(xsrc + (size_t)n * a.H * a.W * xst);
       const int od = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * a.cout * 4);
-      const int ox = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * cin * 4);
+      const int ox = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * xst * 4);
 #pragma unroll
       for (int k = 0; k < WX_DI; ++k) dv[k] = bld4(rd, co_ok ? ld_d[k] + od : WX_OOB, 0);
       unsigned m = 0;
@@ -753,7 +756,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
   constexpr int NTAP = 9;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
   f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop
-  const int cin = a.c0;
+  const int cin = a.c0 + a.c1;  // (X = concat(x0[c0], x1[c1]): a 64-channel tile never straddles them)
   const int nci = (cin + 63) / 64;
   int tile = blockIdx.x, zs = blockIdx.y;
   if ((gridDim.y & 7) == 0) {  // the tiles of one z on one XCD (wgrad_x3_kernel)
@@ -763,6 +766,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
   }
   const int cit = tile % nci, cot = tile / nci;
   const int co0 = cot * 64, ci0 = cit * 64;
+  const bool src1 = a.c1 && ci0 >= a.c0;  // the tile's X source (block-uniform), its row stride, channel base
+  const float* const xsrc = src1 ? a.x1 : a.x0;
+  const int xst = src1 ? a.c1 : a.c0, xc0 = src1 ? ci0 - a.c0 : ci0;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool producer = wave >= 4;
@@ -800,7 +806,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
         const int hp = (ptid + WS_NTP * k) >> 4;
         xhy[k] = hp < HP ? hp / HWc - 1 : -1000000;
         xhx[k] = hp % HWc - 1;
-        ld_x[k] = hp < HP ? ((xhy[k] * a.W + xhx[k]) * cin + ci0 + 4 * cq) * 4 : 0;
+        ld_x[k] = hp < HP ? ((xhy[k] * a.W + xhx[k]) * xst + xc0 + 4 * cq) * 4 : 0;
       }
 #pragma unroll
       for (int k = 0; k < DI; ++k) {
@@ -813,9 +819,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
         int n, y0, x0;
         chunk_origin(c, n, y0, x0);
         const rsrc_t rd = mkrsrc(a.dy + (size_t)n * a.H * a.W * a.cout);
-        const rsrc_t rx = mkrsrc(a.x0 + (size_t)n * a.H * a.W * cin);
+        const rsrc_t rx = mkrsrc(xsrc + (size_t)n * a.H * a.W * xst);
         const int od = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * a.cout * 4);
-        const int ox = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * cin * 4);
+        const int ox = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * xst * 4);
 #pragma unroll
         for (int k = 0; k < DI; ++k) dvs[S][k] = bld4(rd, co_ok ? ld_d[k] + od : WX_OOB, 0);
         unsigned m = 0;
@@ -1274,7 +1280,18 @@ struct GnBwdArgs {
   const float* dout; const float* x; int N, HW, C;
   const float* gamma; const float* beta; const float* ss; int ss_stride; int act_silu;
   const float* stats;
+  // x = concat(x[C0], x1[C - C0]) (the output blocks' skip concat, read by channel range); C0 = C: one tensor
+  const float* x1; int C0;
 };
+// the thread's x quad (channels c0 .. c0 + 3 of image n): base pointer and pixel stride in its source
+__device__ __forceinline__ const float* gn_xsrc(const GnBwdArgs& a, int n, int c0, int& stride) {
+  if (c0 < a.C0) {
+    stride = a.C0;
+    return a.x + (int64_t)n * a.HW * a.C0 + c0;
+  }
+  stride = a.C - a.C0;
+  return a.x1 + (int64_t)n * a.HW * stride + (c0 - a.C0);
+}
 // grid (slices, N), 256 threads laid out as gn_stat_partial_kernel's (row, channel quad); a thread's
 // per-channel coefficients stay in registers
 __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnBwdArgs a, float* __restrict__ part) {
@@ -1299,8 +1316,10 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnBwdArgs a, float*
     }
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, s3[4] = {0.f, 0.f, 0.f, 0.f};
     const int64_t base = (int64_t)n * a.HW * C + c0;
+    int xs;
+    const float* const xb = gn_xsrc(a, n, c0, xs);
     for (int p = p0 + r; p < p1; p += R) {
-      const f32x4 xv = *reinterpret_cast<const f32x4*>(a.x + base + (int64_t)p * C);
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + (int64_t)p * xs);
       const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dout + base + (int64_t)p * C);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1410,10 +1429,12 @@ __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(GnBwdArgs a, const float
     r1[j] = red[(n * 32 + g) * 2 + 1];
   }
   const int64_t base = (int64_t)n * a.HW * C + c0;
+  int xs;
+  const float* const xb = gn_xsrc(a, n, c0, xs);
 #pragma unroll 2
   for (int p = p0 + r; p < p1; p += R) {
     const int64_t i = base + (int64_t)p * C;
-    const f32x4 xv = *reinterpret_cast<const f32x4*>(a.x + i);
+    const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + (int64_t)p * xs);
     const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dout + i);
     f32x4 prev = {0.f, 0.f, 0.f, 0.f};
     if (accumulate) prev = *reinterpret_cast<const f32x4*>(dx + i);
@@ -2148,8 +2169,8 @@ static void conv_x3_params(ConvParams& p, const float* x0, int c0, const float* 
   conv_params(p, x0, c0, x1, c1, N, H, (const float*)wx3, bias, cin_pad, cout, cout, 64, 9, res, out);
   p.opt_bm128 = 0;
   p.x3_nprod = 3;
-  if (taps == 1) {
-    p.s0 = x0; p.sc0 = c0; p.s1 = nullptr; p.sc1 = 0;
+  if (taps == 1) {  // (two sources: the output blocks' concat, read by channel range)
+    p.s0 = x0; p.sc0 = c0; p.s1 = c1 ? x1 : nullptr; p.sc1 = c1;
     p.wskip = (const float*)wx3; p.cs_pad = cin_pad;
     p.in0 = nullptr; p.c0 = 0; p.in1 = nullptr; p.c1 = 0; p.cin_pad = 0;
     conv_geometry(p, H, H, N, 64, cin_pad / 32, true);
@@ -2187,8 +2208,8 @@ static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, 
   }
   ConvParams p;
   const int taps = wx3_taps;
-  if (taps == 1 && (c1 || cin_pad % 32)) {
-    set_error("ifd_tr_conv_x3: 1x1 needs one input with cin % 32 == 0");
+  if (taps == 1 && (c0 % 32 || c1 % 32 || (c1 && !x1))) {
+    set_error("ifd_tr_conv_x3: 1x1 needs input channel counts % 32 == 0");
     return 3;
   }
   if (actA && (taps != 9 || !actB)) {  // (the 1x1 operand goes to LDS by DMA, unactivated)
@@ -2344,9 +2365,12 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
   return TR_LAST();
 }
 
-static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int N, int H, int taps,
-                        const float* actA, const float* actB, float* dw, float* db, float* part, int64_t part_floats,
-                        float* colpart, int64_t colpart_floats, unsigned* guard, int nprod, void* stream);
+static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                        int taps, const float* actA, const float* actB, float* dw, float* db, float* part,
+                        int64_t part_floats, float* colpart, int64_t colpart_floats, unsigned* guard, int nprod,
+                        void* stream);
+// two sources (the output blocks' concat): the split kernels read a 64-channel input tile from one of them
+static bool wgrad_x3_srcs_ok(const float* x1, int c0, int c1) { return !c1 || (x1 && c0 % 64 == 0 && c1 % 4 == 0); }
 
 int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                          int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
@@ -2354,45 +2378,50 @@ int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, con
   // the split kernel: 3x3 or 1x1, one input tensor, power-of-two maps >= 8, channel counts in 16-B quads
   // (its staging loads four channels at a time); else fp32
   // (and images within a buffer descriptor's 2 GB range: the staging loads address one image each)
-  if ((taps != 9 && taps != 1) || c1 || H < 8 || (H & (H - 1)) || !guard || cout % 4 || c0 % 4 ||
-      (int64_t)H * H * (cout > c0 ? cout : c0) * 4 >= 0x7ffffff0)
+  const int cmax = cout > c0 + c1 ? cout : c0 + c1;
+  if ((taps != 9 && taps != 1) || !wgrad_x3_srcs_ok(x1, c0, c1) || H < 8 || (H & (H - 1)) || !guard || cout % 4 ||
+      c0 % 4 || (int64_t)H * H * cmax * 4 >= 0x7ffffff0)
     return ifd_tr_conv_wgrad(dy, cout, x0, c0, x1, c1, N, H, taps, dw, db, part, part_floats, colpart, colpart_floats,
                              stream);
-  return wgrad_x3_run(dy, cout, x0, c0, N, H, taps, nullptr, nullptr, dw, db, part, part_floats, colpart,
+  return wgrad_x3_run(dy, cout, x0, c0, x1, c1, N, H, taps, nullptr, nullptr, dw, db, part, part_floats, colpart,
                       colpart_floats, guard, nprod, stream);
 }
 
-int ifd_tr_conv_wgrad_x3_gn(const float* dy, int cout, const float* x0, int c0, int N, int H, const float* actA,
-                            const float* actB, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
-                            int64_t colpart_floats, unsigned* guard, int nprod, void* stream) {
-  if (!actA || !actB || H < 8 || (H & (H - 1)) || !guard || cout % 4 || c0 % 4 ||
-      (int64_t)H * H * (cout > c0 ? cout : c0) * 4 >= 0x7ffffff0) {
+int ifd_tr_conv_wgrad_x3_gn(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                            const float* actA, const float* actB, float* dw, float* db, float* part,
+                            int64_t part_floats, float* colpart, int64_t colpart_floats, unsigned* guard, int nprod,
+                            void* stream) {
+  const int cmax = cout > c0 + c1 ? cout : c0 + c1;
+  if (!actA || !actB || !wgrad_x3_srcs_ok(x1, c0, c1) || H < 8 || (H & (H - 1)) || !guard || cout % 4 || c0 % 4 ||
+      (int64_t)H * H * cmax * 4 >= 0x7ffffff0) {
     set_error("ifd_tr_conv_wgrad_x3_gn: shape not eligible for the split kernel (materialise the activation)");
     return 3;
   }
-  return wgrad_x3_run(dy, cout, x0, c0, N, H, 9, actA, actB, dw, db, part, part_floats, colpart, colpart_floats,
-                      guard, nprod, stream);
+  return wgrad_x3_run(dy, cout, x0, c0, x1, c1, N, H, 9, actA, actB, dw, db, part, part_floats, colpart,
+                      colpart_floats, guard, nprod, stream);
 }
 
-static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int N, int H, int taps,
-                        const float* actA, const float* actB, float* dw, float* db, float* part, int64_t part_floats,
-                        float* colpart, int64_t colpart_floats, unsigned* guard, int nprod, void* stream) {
+static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                        int taps, const float* actA, const float* actB, float* dw, float* db, float* part,
+                        int64_t part_floats, float* colpart, int64_t colpart_floats, unsigned* guard, int nprod,
+                        void* stream) {
   const int64_t P = (int64_t)N * H * H;
+  const int cin = c0 + c1;
   int S = 1;
-  const int64_t need = ifd_tr_wgrad_part_floats(cout, c0, taps, P, &S);
+  const int64_t need = ifd_tr_wgrad_part_floats(cout, cin, taps, P, &S);
   if (!dy || !x0 || !dw || !part || need > part_floats || (nprod != 1 && nprod != 3)) {
     set_error("ifd_tr_conv_wgrad_x3: bad arguments or workspace too small");
     return 2;
   }
   WgArgs a;
-  a.dy = dy; a.cout = cout; a.x0 = x0; a.c0 = c0; a.x1 = x0; a.c1 = 0;
+  a.dy = dy; a.cout = cout; a.x0 = x0; a.c0 = c0; a.x1 = c1 ? x1 : x0; a.c1 = c1;
   a.N = N; a.H = H; a.W = H; a.taps = taps; a.P = P;
   a.part = part;
   a.actA = actA; a.actB = actB;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nch = P / WX_PX;
   a.chunks_per_split = (int)((nch + S - 1) / S);
-  const int tiles = ((cout + 63) / 64) * ((c0 + 63) / 64);
+  const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64);
   // bias gradient fused into the kernel when the column-sum workspace holds one row per split
   const bool fused_db = db && colpart && (int64_t)S * cout <= colpart_floats && cout % 4 == 0;
   float* cp = fused_db ? colpart : nullptr;
@@ -2414,7 +2443,7 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, int 
     hipLaunchKernelGGL((wgrad_x3_kernel<1, 3, false>), g9, b1, 0, s, a, guard, cp);
   else
     hipLaunchKernelGGL((wgrad_x3_kernel<1, 1, false>), g9, b1, 0, s, a, guard, cp);
-  const int64_t n = (int64_t)cout * c0 * taps;
+  const int64_t n = (int64_t)cout * cin * taps;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (fused_db) {
     hipLaunchKernelGGL(colsum_final_kernel, dim3((cout + 63) / 64), dim3(64), 0, s, colpart, S, cout, db, 1);
@@ -2506,13 +2535,21 @@ int ifd_tr_act_apply(const float* x, int N, int HW, int C, const float* A, const
 int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
                   const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
                   float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream) {
+  return ifd_tr_gn_bwd_cat(dout, x, C, nullptr, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, dx, accumulate,
+                           dgamma, dbeta, dss, work, work_floats, stream);
+}
+
+int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
+                      const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
+                      const float* stats, float* dx, int accumulate, float* dgamma, float* dbeta, float* dss,
+                      float* work, int64_t work_floats, void* stream) {
   const int nsl = gn_nsl(HW, N, C);
   const int64_t need = (int64_t)N * nsl * C * 3 + (int64_t)N * C * 3 + (int64_t)N * 64;
-  if (C % 32 || C > 1024 || need > work_floats) {
-    set_error("ifd_tr_gn_bwd: C must be a multiple of 32 (<= 1024); work too small");
+  if (C % 32 || C > 1024 || need > work_floats || C0 % 4 || C0 <= 0 || C0 > C || (C0 < C && !x1)) {
+    set_error("ifd_tr_gn_bwd: C must be a multiple of 32 (<= 1024), 0 < C0 <= C in quads; work too small");
     return 2;
   }
-  GnBwdArgs a{dout, x, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats};
+  GnBwdArgs a{dout, x0, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, x1, C0};
   float* part = work;
   float* nc = work + (int64_t)N * nsl * C * 3;
   float* red = nc + (int64_t)N * C * 3;

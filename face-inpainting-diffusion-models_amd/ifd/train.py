@@ -46,7 +46,10 @@ TRAIN_EXPORTS = {
                                 vp, vp, i32, vp]),
     "ifd_tr_conv_gn": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, i64,
                              vp]),
-    "ifd_tr_conv_wgrad_x3_gn": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp, i64, vp, i32, vp]),
+    "ifd_tr_conv_wgrad_x3_gn": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp, i64, vp, i32,
+                                      vp]),
+    "ifd_tr_gn_bwd_cat": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, i64,
+                                vp]),
     "ifd_tr_gn_slices": (i64, [i32, i32, i32]),
     "ifd_tr_gn_coef": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, i32, f32, vp, vp, vp, vp, i64, vp]),
     "ifd_tr_act_apply": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp]),
@@ -259,7 +262,7 @@ class UNetTrainer:
             return None
         if taps == 9 and (ppad // 64) & (ppad // 64 - 1):
             return None
-        if taps == 1 and (pout % 64 or c1 or cin_x != pin or cin_x % 32):
+        if taps == 1 and (pout % 64 or cin_x + c1 != pin or cin_x % 32 or c1 % 32):
             return None
         cin_pad = cin_x + c1
         key = (name, int(transpose), "x3")
@@ -352,46 +355,57 @@ class UNetTrainer:
                               P(out), P(part), pf, self.s))
         return out
 
-    def wgrad(self, dy, cout, x, cin_x, N, H, name, bias_name=None, real_cin=None, gn=None):
-        """grad[name] += conv weight gradient; grad[bias] += column sums of dy.
+    def wgrad(self, dy, cout, x, cin_x, N, H, name, bias_name=None, real_cin=None, gn=None, x1=None, c1=0):
+        """grad[name] += conv weight gradient; grad[bias] += column sums of dy. The input is concat(x[cin_x],
+        x1[c1]) (the output blocks' skip concat, never materialised).
         gn = (A, B): the forward conv's input was silu(A x + B) of the raw x (recomputed at staging, or
         materialised here when the split kernel does not take the shape)."""
         w = self.p(name)
         taps = int(np.prod(w.shape[2:])) if w.dim() > 2 else 1
         P_ = N * H * H
+        cin = cin_x + c1
         S = _c.c_int()
-        need = lib().ifd_tr_wgrad_part_floats(cout, cin_x, taps, P_, _c.byref(S))
+        need = lib().ifd_tr_wgrad_part_floats(cout, cin, taps, P_, _c.byref(S))
         part = self._empty(need)
         colpart = self._empty(((P_ + 1023) // 1024) * cout)
         real_cin = real_cin or w.shape[1]
         real_cout = w.shape[0]
-        direct = real_cin == cin_x and real_cout == cout
-        dw = self.g(name) if direct else self._zeros(cout * cin_x * taps)
+        direct = real_cin == cin and real_cout == cout
+        dw = self.g(name) if direct else self._zeros(cout * cin * taps)
         db = self.g(bias_name) if (bias_name and real_cout == cout) else (self._zeros(cout) if bias_name else None)
         rc = 3
         if gn is not None and self._split() and self.x3_wgrad and taps == 9:
-            rc = lib().ifd_tr_conv_wgrad_x3_gn(P(dy), cout, P(x), cin_x, N, H, P(gn[0]), P(gn[1]), P(dw), P(db),
-                                               P(part), need, P(colpart), colpart.numel(), P(self._guard),
+            rc = lib().ifd_tr_conv_wgrad_x3_gn(P(dy), cout, P(x), cin_x, P(x1), c1, N, H, P(gn[0]), P(gn[1]), P(dw),
+                                               P(db), P(part), need, P(colpart), colpart.numel(), P(self._guard),
                                                self._nprod(), self.s)
         if rc != 3:
             chk(rc)
         else:
             if gn is not None:  # the split kernel does not take this shape: materialise the activation
+                if x1 is not None:
+                    x, cin_x, x1, c1 = self._cat(x, cin_x, x1, c1, N * H * H), cin, None, 0
                 x = self.act_apply(x, N, H * H, cin_x, gn)
-            self._wgrad_plain(dy, cout, x, cin_x, N, H, taps, dw, db, part, need, colpart)
+            self._wgrad_plain(dy, cout, x, cin_x, x1, c1, N, H, taps, dw, db, part, need, colpart)
         if not direct:  # padded input (the first conv reads 16 channels, 9 real) or output (head: 8, 6 real)
-            chk(lib().ifd_tr_copy_channels(P(dw), cin_x * taps, 0, P(self.g(name)), real_cin * taps, 0, real_cin * taps,
+            chk(lib().ifd_tr_copy_channels(P(dw), cin * taps, 0, P(self.g(name)), real_cin * taps, 0, real_cin * taps,
                                            real_cout, 1, self.s))
         if bias_name and real_cout != cout:
             chk(lib().ifd_tr_copy_channels(P(db), cout, 0, P(self.g(bias_name)), real_cout, 0, real_cout, 1, 1, self.s))
 
-    def _wgrad_plain(self, dy, cout, x, cin_x, N, H, taps, dw, db, part, need, colpart):
+    def _wgrad_plain(self, dy, cout, x, cin_x, x1, c1, N, H, taps, dw, db, part, need, colpart):
         if self._split() and self.x3_wgrad:
-            chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
+            chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(x), cin_x, P(x1), c1, N, H, taps, P(dw), P(db), P(part), need,
                                            P(colpart), colpart.numel(), P(self._guard), self._nprod(), self.s))
         else:
-            chk(lib().ifd_tr_conv_wgrad(P(dy), cout, P(x), cin_x, None, 0, N, H, taps, P(dw), P(db), P(part), need,
+            chk(lib().ifd_tr_conv_wgrad(P(dy), cout, P(x), cin_x, P(x1), c1, N, H, taps, P(dw), P(db), P(part), need,
                                         P(colpart), colpart.numel(), self.s))
+
+    def _cat(self, x, cx, x1, c1, npix):
+        """concat(x[cx], x1[c1]) materialised (the paths that cannot read the two sources)."""
+        cat = self._empty(npix * (cx + c1))
+        self.copy_ch(x, cx, 0, cat, cx + c1, 0, cx, npix, False)
+        self.copy_ch(x1, c1, 0, cat, cx + c1, cx, c1, npix, False)
+        return cat
 
     def gn_fwd(self, x, N, HW, C, prefix, ss=None, ss_stride=0, silu=True):
         out = self._empty(N * HW * C)
@@ -411,11 +425,23 @@ class UNetTrainer:
     def _gn_fused(self):
         return self.fuse_gn and self._split()
 
-    def gn_coef(self, x, N, HW, C, prefix, ss=None, ss_stride=0):
-        """(A, B), stats of GroupNorm + scale/shift for a consumer that applies silu(A x + B) on load."""
+    def _granules2(self, x, x1):
+        """The producing convs' granule statistics of concat(x, x1) as one record, or None."""
+        ga, gb = self._gstat.get(x.data_ptr()), self._gstat.get(x1.data_ptr())
+        if (ga is not None and gb is not None and ga[0] is x and gb[0] is x1 and ga[5] is None and gb[5] is None
+                and ga[2:4] == gb[2:4]):
+            return (None, ga[1], ga[2], ga[3], ga[4], gb[1])
+        return None
+
+    def gn_coef(self, x, N, HW, C, prefix, ss=None, ss_stride=0, x1=None):
+        """(A, B), stats of GroupNorm + scale/shift for a consumer that applies silu(A x + B) on load.
+        x1: the concat's second source (granule statistics of both are required)."""
         A, B = self._empty(N, C), self._empty(N, C)
         stats = self._empty(N * 64)
-        g = self._gstat.get(x.data_ptr())
+        g = self._granules2(x, x1) if x1 is not None else self._gstat.get(x.data_ptr())
+        if x1 is not None:
+            assert g is not None and C % 128 == 0, "a concat GroupNorm on load needs both sources' granules"
+            g = (x,) + g[1:]
         gam, bet = self.p(prefix + "weight"), self.p(prefix + "bias")
         if g is not None and g[0] is x and C % 128 == 0:
             chk(lib().ifd_tr_gn_coef(None, N, HW, C, P(gam), P(bet), P(ss), ss_stride, P(g[1]), g[4], P(g[5]), g[2],
@@ -432,7 +458,9 @@ class UNetTrainer:
         chk(lib().ifd_tr_act_apply(P(x), N, HW, C, P(gn[0]), P(gn[1]), int(silu), P(out), self.s))
         return out
 
-    def gn_bwd(self, dout, x, N, HW, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None, silu=True):
+    def gn_bwd(self, dout, x, N, HW, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None, silu=True, x1=None,
+               C0=None):
+        """x1, C0: the GroupNorm input is concat(x[C0], x1[C - C0]) (read by channel range)."""
         acc = dx is not None
         if dx is None:
             dx = self._empty(N * HW * C)
@@ -440,9 +468,10 @@ class UNetTrainer:
             self._dirty(dx)
         nsl = lib().ifd_tr_gn_slices(HW, N, C)
         work = self._empty(N * nsl * C * 3 + N * C * 3 + N * 64)
-        chk(lib().ifd_tr_gn_bwd(P(dout), P(x), N, HW, C, P(self.p(prefix + "weight")), P(self.p(prefix + "bias")),
-                                P(ss), ss_stride, int(silu), P(stats), P(dx), int(acc), P(self.g(prefix + "weight")),
-                                P(self.g(prefix + "bias")), P(dss), P(work), work.numel(), self.s))
+        chk(lib().ifd_tr_gn_bwd_cat(P(dout), P(x), C0 if x1 is not None else C, P(x1), N, HW, C,
+                                    P(self.p(prefix + "weight")), P(self.p(prefix + "bias")), P(ss), ss_stride,
+                                    int(silu), P(stats), P(dx), int(acc), P(self.g(prefix + "weight")),
+                                    P(self.g(prefix + "bias")), P(dss), P(work), work.numel(), self.s))
         return dx
 
     def resample(self, x, N, Hin, C, mode):
@@ -506,25 +535,34 @@ class UNetTrainer:
         hs, saved = [], {}
         h, hc, hr = None, 0, H
         for section, bi, layers in self.plan:
+            pend = None  # the output block's skip, read by the block's first ResBlock as concat(h, skip)
             if section == "output":
                 skip = hs.pop()
                 sc = skip.shape[-1]
-                cat = self._empty(N, hr, hr, hc + sc)
-                self.copy_ch(h, hc, 0, cat, hc + sc, 0, hc, N * hr * hr, False)
-                self.copy_ch(skip, sc, 0, cat, hc + sc, hc, sc, N * hr * hr, False)
-                # the concat's GroupNorm statistics from both sources' granules (same map: same E, cnt)
-                ga, gb = self._gstat.get(h.data_ptr()), self._gstat.get(skip.data_ptr())
-                if (ga is not None and gb is not None and ga[0] is h and gb[0] is skip and ga[5] is None
-                        and gb[5] is None and ga[2:4] == gb[2:4]):
-                    self._gstat[cat.data_ptr()] = (cat, ga[1], ga[2], ga[3], hc, gb[1])
-                h, hc = cat, hc + sc
+                L0 = layers[0]
+                if (self._gn_fused() and L0["kind"] == "res" and L0["cout"] != hc + sc and hc % 64 == 0
+                        and sc % 32 == 0 and (hc + sc) % 128 == 0 and self._granules2(h, skip) is not None):
+                    pend = (skip, sc)
+                else:  # the concat materialised (code/unet.py:170)
+                    cat = self._empty(N, hr, hr, hc + sc)
+                    self.copy_ch(h, hc, 0, cat, hc + sc, 0, hc, N * hr * hr, False)
+                    self.copy_ch(skip, sc, 0, cat, hc + sc, hc, sc, N * hr * hr, False)
+                    # the concat's GroupNorm statistics from both sources' granules (same map: same E, cnt)
+                    g2 = self._granules2(h, skip)
+                    if g2 is not None:
+                        self._gstat[cat.data_ptr()] = (cat,) + g2[1:]
+                    h, hc = cat, hc + sc
             for L in layers:
                 k, p = L["kind"], L["prefix"]
                 if k == "conv_in":
                     h = self.conv(x16, 16, N, hr, p + "weight", p + "bias")
                     hc = L["cout"]
                 elif k in ("res", "res_down", "res_up"):
-                    h, hr = self._res_fwd(L, h, N, hr, emb, saved)
+                    if pend is not None:
+                        h, hr = self._res_fwd(L, h, N, hr, emb, saved, x1=pend[0], c1=pend[1])
+                        pend = None
+                    else:
+                        h, hr = self._res_fwd(L, h, N, hr, emb, saved)
                     hc = L["cout"]
                 elif k == "attn":
                     h = self._attn_fwd(L, h, N, hr, saved)
@@ -544,14 +582,20 @@ class UNetTrainer:
         self._tape = tape
         return h  # [N, H, W, 8]: the 6 output channels, then 2 zero channels
 
-    def _res_fwd(self, L, x, N, r, emb, saved):
-        """ResBlock._forward (code/nn.py:189-212), scale-shift norm, resblock_updown."""
+    def _res_fwd(self, L, x, N, r, emb, saved, x1=None, c1=0):
+        """ResBlock._forward (code/nn.py:189-212), scale-shift norm, resblock_updown. x1: the output blocks'
+        skip tensor; the block's input is then concat(x, x1) (code/unet.py:170), read by channel range by every
+        consumer (GroupNorm statistics from both sources' granules, conv1's prologue, the 1x1 skip conv)."""
         p, cin, cout, k = L["prefix"], L["cin"], L["cout"], L["kind"]
         mode = 1 if k == "res_up" else (2 if k == "res_down" else 0)
         ro = 2 * r if mode == 1 else (r // 2 if mode == 2 else r)
         fused = self._gn_fused()
         g1 = g2 = a1r = a2 = None
-        if fused and not mode:  # in_layers: GroupNorm + SiLU applied by conv1's prologue (and wgrad's staging)
+        c0 = cin - c1
+        if x1 is not None:  # (the caller checked: fused mode, mode 0, cin != cout, both granules)
+            g1, st1 = self.gn_coef(x, N, r * r, cin, p + "in_layers.0.", x1=x1)
+            h1 = self.conv(x, c0, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias", x1=x1, c1=c1, gn=g1)
+        elif fused and not mode:  # in_layers: GroupNorm + SiLU applied by conv1's prologue (and wgrad's staging)
             g1, st1 = self.gn_coef(x, N, r * r, cin, p + "in_layers.0.")
             h1 = self.conv(x, cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias", gn=g1)
         else:
@@ -561,7 +605,7 @@ class UNetTrainer:
         xr = self.resample(x, N, r, cin, mode) if mode else x
         E = self.linear(emb, N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True)  # [N, 2 cout]
         if cin != cout:
-            skip = self.conv(xr, cin, N, ro, p + "skip_connection.weight", p + "skip_connection.bias")
+            skip = self.conv(xr, c0, N, ro, p + "skip_connection.weight", p + "skip_connection.bias", x1=x1, c1=c1)
         else:
             skip = xr
         if fused:  # out_layers: GroupNorm + scale/shift + SiLU in conv2's prologue
@@ -570,8 +614,8 @@ class UNetTrainer:
         else:
             a2, st2 = self.gn_fwd(h1, N, ro * ro, cout, p + "out_layers.0.", ss=E, ss_stride=2 * cout, silu=True)
             out = self.conv(a2, cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias", res=skip)
-        saved[p] = dict(x=x, a1r=a1r, g1=g1, xr=xr, h1=h1, a2=a2, g2=g2, E=E, st1=st1, st2=st2, mode=mode, r=r,
-                        ro=ro)
+        saved[p] = dict(x=x, x1=x1, c1=c1, a1r=a1r, g1=g1, xr=xr, h1=h1, a2=a2, g2=g2, E=E, st1=st1, st2=st2,
+                        mode=mode, r=r, ro=ro)
         return out, ro
 
     def _attn_fwd(self, L, x, N, r, saved):
@@ -697,14 +741,18 @@ class UNetTrainer:
                           ss_stride=2 * cout, dss=dE, silu=True)
         self.linear_bwd(dE, self._tape["emb"], N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True,
                         dx=demb)
+        x1, c1 = sv.get("x1"), sv.get("c1", 0)
+        c0 = cin - c1  # (x1: the block input is concat(x[c0], x1[c1]), never materialised)
         if sv["g1"] is not None:
-            self.wgrad(dh1, cout, sv["x"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias", gn=sv["g1"])
+            self.wgrad(dh1, cout, sv["x"], c0, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias", gn=sv["g1"],
+                       x1=x1, c1=c1)
         else:
             self.wgrad(dh1, cout, sv["a1r"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
         da1r = self.conv(dh1, cout, N, ro, p + "in_layers.2.weight", transpose=True)
         da1 = self.resample_bwd(da1r, N, r, cin, mode) if mode else da1r
         if cin != cout:
-            self.wgrad(dout, cout, sv["xr"], cin, N, ro, p + "skip_connection.weight", p + "skip_connection.bias")
+            self.wgrad(dout, cout, sv["xr"], c0, N, ro, p + "skip_connection.weight", p + "skip_connection.bias",
+                       x1=x1, c1=c1)
             dxr = self.conv(dout, cout, N, ro, p + "skip_connection.weight", transpose=True)
         else:
             dxr = dout
@@ -714,7 +762,8 @@ class UNetTrainer:
         else:
             # the skip path's gradient (dout itself, or the 1x1 conv's fresh dgrad) is the accumulation
             # target of the GroupNorm input gradient: no separate add pass
-            dx = self.gn_bwd(da1, sv["x"], N, r * r, cin, p + "in_layers.0.", sv["st1"], dx=dxr, silu=True)
+            dx = self.gn_bwd(da1, sv["x"], N, r * r, cin, p + "in_layers.0.", sv["st1"], dx=dxr, silu=True, x1=x1,
+                             C0=c0)
         return dx, r
 
     # ------------------------------------------------------------------ loss / step

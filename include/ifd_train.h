@@ -92,19 +92,21 @@ int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* sp
 int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                       int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
                       int64_t colpart_floats, void* stream);
-/* ifd_tr_conv_wgrad with the 3xf16 split kernel for 3x3 convs of one input tensor on maps >= 8x8 (both
+/* ifd_tr_conv_wgrad with the 3xf16 split kernel for 3x3 / 1x1 convs on maps >= 8x8, X = concat(x0, x1) with
+ * c0 % 64 == 0 when c1 > 0 (both
  * operands split on the fly, three f16 products per MAC, fp32 accumulation; |operand| >= 65504 sets bit 1
  * of *guard); other shapes run ifd_tr_conv_wgrad. Same workspaces. nprod 1: the hi x hi product only (the
  * reduced-precision f16 training mode). */
 int ifd_tr_conv_wgrad_x3(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
                          int taps, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
                          int64_t colpart_floats, unsigned* guard, int nprod, void* stream);
-/* ifd_tr_conv_wgrad_x3 (3x3) of the weight whose forward ran ifd_tr_conv_x3_gn: X = silu(actA x0 + actB),
- * recomputed at staging from the raw x0. Returns 3 (nothing launched) for shapes the split kernel does not
+/* ifd_tr_conv_wgrad_x3 (3x3) of the weight whose forward ran ifd_tr_conv_x3_gn: X = silu(actA x + actB),
+ * recomputed at staging from the raw x = concat(x0[c0], x1[c1]) (c1 > 0: c0 % 64 == 0). Returns 3 (nothing launched) for shapes the split kernel does not
  * take: the caller then materialises X (ifd_tr_act_apply) and calls ifd_tr_conv_wgrad[_x3]. */
-int ifd_tr_conv_wgrad_x3_gn(const float* dy, int cout, const float* x0, int c0, int N, int H, const float* actA,
-                            const float* actB, float* dw, float* db, float* part, int64_t part_floats, float* colpart,
-                            int64_t colpart_floats, unsigned* guard, int nprod, void* stream);
+int ifd_tr_conv_wgrad_x3_gn(const float* dy, int cout, const float* x0, int c0, const float* x1, int c1, int N, int H,
+                            const float* actA, const float* actB, float* dw, float* db, float* part,
+                            int64_t part_floats, float* colpart, int64_t colpart_floats, unsigned* guard, int nprod,
+                            void* stream);
 /* GroupNorm statistics and apply coefficients without the apply pass: stats[n][32][2] = (mean, rstd) as
  * ifd_tr_gn_fwd's, A[n][c] = rstd gamma (1 + scale), B[n][c] = (beta - mean rstd gamma)(1 + scale) + shift
  * (ss as ifd_tr_gn_fwd's, or NULL). From granules (gstat0 != NULL: ifd_tr_gn_fwd_gstat's contract, x unused)
@@ -135,6 +137,12 @@ int ifd_tr_gn_fwd_gstat(const float* x, int N, int HW, int C, const float* gamma
 int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
                   const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
                   float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream);
+/* ifd_tr_gn_bwd of a concat input x = concat(x0[C0], x1[C - C0]) read by channel range (the output blocks'
+ * cat(h, skip), code/unet.py:170); dx is the concat's gradient as one [N][HW][C] tensor. */
+int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
+                      const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
+                      const float* stats, float* dx, int accumulate, float* dgamma, float* dbeta, float* dss,
+                      float* work, int64_t work_floats, void* stream);
 /* nearest-up x2 (mode 1) / AvgPool2d(2) (mode 2) (code/nn.py:92-133) and the adjoint (dx at Hin). */
 int ifd_tr_resample(const float* x, int N, int Hin, int C, int mode, float* out, void* stream);
 int ifd_tr_resample_bwd(const float* dy, int N, int Hin, int C, int mode, float* dx, int accumulate, void* stream);

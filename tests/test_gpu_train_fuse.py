@@ -187,3 +187,61 @@ def test_head_x3_matches_fp32(N, H, cin, record):
     assert float(out[..., 6:].abs().max()) == 0.0
     r, m = _close(out[..., :6], ref[..., :6])
     record(f"train_fuse/head_x3/{N}x{H}x{cin}", rel_l2=r, max_rel=m)
+
+
+@pytest.mark.parametrize("N,H,c0,c1,cout", [(2, 32, 128, 128, 128), (2, 16, 256, 64, 256)])
+def test_concat_sources_match_materialised(N, H, c0, c1, cout, record):
+    """The output blocks' concat read by channel range (UNetTrainer: the skip concat is never written):
+    the GroupNorm backward (ifd_tr_gn_bwd_cat), the 3x3 weight gradient with the GroupNorm prologue and the
+    1x1 weight gradient on two sources vs the same ops on the materialised concat: bit-identical."""
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    C = c0 + c1
+    g = torch.Generator().manual_seed(N + H + c0 + c1)
+    xa = (torch.randn(N, H, H, c0, generator=g) + 0.2).to(DEV)
+    xb = (torch.randn(N, H, H, c1, generator=g) - 0.1).to(DEV)
+    cat = torch.cat([xa, xb], dim=-1).contiguous()
+    dy = torch.randn(N, H, H, cout, generator=g).to(DEV)
+    A, B, st, _, _ = _coef(cat, N, H * H, C, seed=2)
+    guard = torch.zeros(4, device=DEV, dtype=torch.int32)
+    P_ = N * H * H
+    res = {}
+    for taps in (9, 1):
+        S = ctypes.c_int()
+        need = lib().ifd_tr_wgrad_part_floats(cout, C, taps, P_, ctypes.byref(S))
+        part = torch.empty(need, device=DEV)
+        colpart = torch.empty(((P_ + 1023) // 1024) * cout, device=DEV)
+        outs = []
+        for two in (False, True):
+            dw, db = torch.zeros(cout * C * taps, device=DEV), torch.zeros(cout, device=DEV)
+            x0, cc0, x1, cc1 = (xa, c0, xb, c1) if two else (cat, C, None, 0)
+            if taps == 9:
+                chk(lib().ifd_tr_conv_wgrad_x3_gn(P(dy), cout, P(x0), cc0, P(x1), cc1, N, H, P(A), P(B), P(dw), P(db),
+                                                  P(part), need, P(colpart), colpart.numel(), P(guard), 3, s))
+            else:
+                chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(x0), cc0, P(x1), cc1, N, H, 1, P(dw), P(db), P(part),
+                                               need, P(colpart), colpart.numel(), P(guard), 3, s))
+            outs.append((dw, db))
+        res[taps] = outs
+    gamma = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    da = torch.randn(N, H, H, C, generator=g).to(DEV)
+    nsl = lib().ifd_tr_gn_slices(H * H, N, C)
+    gx = []
+    for two in (False, True):
+        dx = torch.empty(N, H, H, C, device=DEV)
+        dgam, dbet = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        work = torch.empty(N * nsl * C * 3 + N * C * 3 + N * 64, device=DEV)
+        x0, cc0, x1 = (xa, c0, xb) if two else (cat, C, None)
+        chk(lib().ifd_tr_gn_bwd_cat(P(da), P(x0), cc0, P(x1), N, H * H, C, P(gamma), P(beta), None, 0, 1, P(st), P(dx),
+                                    0, P(dgam), P(dbet), None, P(work), work.numel(), s))
+        gx.append((dx, dgam, dbet))
+    torch.cuda.synchronize()
+    assert int(guard.max()) == 0
+    for taps in (9, 1):
+        assert torch.equal(res[taps][0][0], res[taps][1][0]) and torch.equal(res[taps][0][1], res[taps][1][1]), taps
+    for a, b in zip(gx[0], gx[1]):
+        assert torch.equal(a, b)
+    record(f"train_fuse/concat_sources/{N}x{H}x{c0}+{c1}->{cout}", bit_identical=True)
