@@ -122,8 +122,8 @@ def test_wgrad_x3_gn_matches_materialised(N, H, cin, cout, record):
     dw1, db1 = torch.zeros_like(dw0), torch.zeros_like(db0)
     chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(a), cin, None, 0, N, H, 9, P(dw0), P(db0), P(part), need,
                                    P(colpart), colpart.numel(), P(guard), 3, s))
-    chk(lib().ifd_tr_conv_wgrad_x3_gn(P(dy), cout, P(x), cin, N, H, P(A), P(B), P(dw1), P(db1), P(part), need,
-                                      P(colpart), colpart.numel(), P(guard), 3, s))
+    chk(lib().ifd_tr_conv_wgrad_x3_gn(P(dy), cout, P(x), cin, None, 0, N, H, P(A), P(B), P(dw1), P(db1), P(part),
+                                      need, P(colpart), colpart.numel(), P(guard), 3, s))
     torch.cuda.synchronize()
     assert int(guard.max()) == 0
     assert torch.equal(db0, db1)
