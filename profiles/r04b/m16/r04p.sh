@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 4: 16x16x32 conv_x3 consumer variants (double-buffered B, one accumulator), same-box interleaved
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out; mkdir -p $OUT
+cd $R
+for rep in 1 2; do
+  for v in new m16a m16b m16c; do
+    if [ $v = new ]; then unset IFD_LIB_PATH; else export IFD_LIB_PATH=$R/tools/abl/libifd_$v.so; fi
+    r=$(QT_N=20 timeout -k 10 120 python tools/quick_time.py 16 3xf16 2>/dev/null | tail -1) || exit 1
+    echo "$v $r" | tee -a $OUT/m16p.txt
+  done
+done
+for v in new m16a m16b m16c; do
+  if [ $v = new ]; then unset IFD_LIB_PATH; else export IFD_LIB_PATH=$R/tools/abl/libifd_$v.so; fi
+  timeout -k 10 120 python tools/layer_prof.py 16 3xf16 > $OUT/lp_$v.txt 2>&1 || exit 1
+  echo "$v $(tail -1 $OUT/lp_$v.txt) | $(grep 'r256 128+0->128 skip0' $OUT/lp_$v.txt | head -1 | cut -c60-)"
+done
