@@ -49,6 +49,16 @@
 #ifndef X3_ABLATE
 #define X3_ABLATE 0
 #endif
+// Cache policy of the epilogue's output stores: nontemporal (NT). A layer's output is read by the next
+// launch, long after it has left the 4 MiB L2 at the 128^2 / 256^2 sizes that dominate; same-box
+// interleaved +0.4 % per UNet eval (17.7 vs 17.8 ms, profiles/r04b/lds/nt.txt). The residual loads'
+// policy (NT as well) measured the same, so they keep the default.
+#ifndef X3_STORE_AUX
+#define X3_STORE_AUX 2
+#endif
+#ifndef X3_RES_AUX
+#define X3_RES_AUX 0
+#endif
 // IFD_TRACE=1 builds: shader-cycle stamps (s_memtime) of the first 16 chunk intervals into
 // ConvParams::trace, 64 slots per block: [j] consumer wave 0 at interval start, [16 + j] after
 // its MFMAs are issued; producer wave 4: [48 + j] after the LDS writes of interval j, [32 + j]
@@ -500,7 +510,7 @@ struct ResSide {
       const int yy = (y0 + ub / TW) >> 1, xx = ((x0 + ub % TW) >> 1) + ((r & 3) >> 1);
       const int s_up = (yy * res_W + xx) * cout4;
       rv[mr][nr][r] = __builtin_bit_cast(
-          float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb[mr] + nr * 128, up ? s_up : s_none, 0));
+          float, __builtin_amdgcn_raw_buffer_load_b32(rr, vb[mr] + nr * 128, up ? s_up : s_none, X3_RES_AUX));
     }
   }
 };
@@ -628,7 +638,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
             acc[mr][nr][r] = x;
             if (X3_ABLATE != 14)
               __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep + nr * 128,
-                                                    roff(r), 0);
+                                                    roff(r), X3_STORE_AUX);
           }
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
         p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values + stores issued
