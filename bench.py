@@ -14,8 +14,17 @@ every rank seeds the device generator identically, so the full-batch draw is the
 and keeps the rank's rows (results independent of the GPU count, at the cost of
 generating N x the rank's noise on-device); the default `device` mode draws per rank (per-rank seeds).
 
+`--noise parity` also builds the model with the handle option `batch_invariant` (split-K and tile choice
+per image, include/ifd.h), so a rank's images come out bit-identical whatever the shard size: with it the
+line is GPU-count-independent as well as seed-consistent (`config.options` records it).
+`--workload dropin` times what a user of the UNCHANGED reference script gets: the same B = 16 DDIM-100 loop
+driven through `model(x, t, masked_image=, mask=)` once per step with the script's own torch algebra
+(code/test_inp_ddim_100.py:470-576, restated in `script_ddim_pass`), instead of one fused library call per
+step; the line carries the fused rate of the same run beside it.
+
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--noise device|parity]
     python bench.py --workload c4 --gpus 8      # configs[3]: 512 images sharded 8 ways (64 per GPU)
+    python bench.py --workload dropin           # the reference script's per-step loop over model()
 """
 from __future__ import annotations
 
@@ -120,16 +129,20 @@ def pmc_traffic(kernel):
     return {"traffic": None}
 
 
+def device_key(hostname, pr):
+    """One GPU's identity: host, device UUID AND PCI domain:bus:device. Both, because a ROCm build may report
+    a non-unique UUID (all zeros) for every device, and PCI IDs alone repeat across hosts."""
+    return (hostname, str(getattr(pr, "uuid", "")),
+            f"{getattr(pr, 'pci_domain_id', '?')}:{getattr(pr, 'pci_bus_id', '?')}:{getattr(pr, 'pci_device_id', '?')}")
+
+
 def distinct_devices(dev):
-    """Number of distinct GPUs the ranks ran on: every rank contributes (hostname, PCI domain:bus:device or
-    UUID) and the unique entries are counted, so multi-node jobs and launchers that give each rank one
-    visible device are counted right (the local torch.cuda.device_count() sees only this process's
-    devices)."""
+    """Number of distinct GPUs the ranks ran on: every rank contributes its device_key and the unique entries
+    are counted, so multi-node jobs and launchers that give each rank one visible device are counted right
+    (the local torch.cuda.device_count() sees only this process's devices)."""
     import socket
     import torch.distributed as dist
-    pr = torch.cuda.get_device_properties(dev)
-    uid = str(getattr(pr, "uuid", "")) or f"{pr.pci_domain_id}:{pr.pci_bus_id}:{pr.pci_device_id}"
-    key = (socket.gethostname(), uid)
+    key = device_key(socket.gethostname(), torch.cuda.get_device_properties(dev))
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return 1
     keys = [None] * dist.get_world_size()
@@ -267,7 +280,8 @@ def ddpm_main(args):
     torch.cuda.set_device(dev)
     parallel.init(device=dev)
     B, H = args.batch, FULL.image_size
-    model = DiffusionInpaintingModel(FULL, device=dev, precision=args.precision)
+    opts = model_options(args)
+    model = DiffusionInpaintingModel(FULL, device=dev, precision=args.precision, options=opts)
     model.load_state_dict(make_state_dict(FULL, seed=1))
     diffusion = create_gaussian_diffusion(steps=args.ddpm_steps, learn_sigma=True, noise_schedule="linear")
     sampler = InpaintingSampler(model, diffusion, device=dev)
@@ -289,6 +303,7 @@ def ddpm_main(args):
     parallel.barrier(dev)
     elapsed = parallel.max_over_ranks(time.perf_counter() - t0, dev)
     assert torch.isfinite(y).all()
+    model.guard_check()  # the lazy range guard of the drop-in loop's forwards (raises on a trip)
     n_evals = diffusion.num_timesteps
     res = {"metric": "256x256 DDPM-1000 inpainted images/sec (BASELINE configs[2], full-step stress)",
            "value": round(B * ws * args.steps / elapsed, 4), "unit": "images/s", "n_gpus": ws, "steps": args.steps,
@@ -309,7 +324,46 @@ def ddpm_main(args):
         print(json.dumps(res), flush=True)
 
 
-def main():
+def model_options(args):
+    """Handle options the run's model is built with: parity mode fixes the conv geometry per image
+    (`batch_invariant`), so a C4 shard of 64 images equals the same images run at any other batch size."""
+    return {"batch_invariant": 1} if args.noise == "parity" else {}
+
+
+def script_ddim_pass(model, alphas_cumprod, shape, gt_images, masks, ddim_steps, eta, device, clip_denoised=True):
+    """The reference script's DDIM loop as it runs unchanged over this library's model
+    (code/test_inp_ddim_100.py:470-576; model_fn :373-385): one `model(x, t, masked_image=, mask=)` per step,
+    the DDIM update and the known-region injection in torch, the per-step alpha tensors built on the device
+    from the float64 table exactly as the script builds them."""
+    img = torch.randn(*shape, device=device)
+    c = 1000 // ddim_steps
+    seq = list(range(0, 1000, c))
+    if seq[-1] != 999:
+        seq.append(999)
+    seq = seq[::-1]
+    gt_keep_mask = 1 - masks
+    for step_idx, timestep in enumerate(seq):
+        t = torch.tensor([timestep] * shape[0], device=device)
+        masked_image = gt_images * gt_keep_mask + torch.zeros_like(gt_images) * (1 - gt_keep_mask)
+        model_output = model(img, t, masked_image=masked_image, mask=1 - gt_keep_mask)
+        noise_pred = model_output[:, :3]
+        alpha_t = torch.tensor(alphas_cumprod[timestep], device=device)
+        alpha_prev = torch.tensor(alphas_cumprod[seq[step_idx + 1]] if step_idx < len(seq) - 1 else 1.0, device=device)
+        pred_x0 = (img - torch.sqrt(1 - alpha_t) * noise_pred) / torch.sqrt(alpha_t)
+        if clip_denoised:
+            pred_x0 = torch.clamp(pred_x0, -1, 1)
+        sigma = eta * torch.sqrt((1 - alpha_prev) / (1 - alpha_t)) * torch.sqrt(1 - alpha_t / alpha_prev)
+        pred_dir = torch.sqrt(1 - alpha_prev - sigma ** 2) * noise_pred
+        noise = torch.randn_like(img) if timestep > 0 and eta > 0 else torch.zeros_like(img)
+        img = torch.sqrt(alpha_prev) * pred_x0 + pred_dir + sigma * noise
+        if timestep > 0:
+            known_noise = torch.randn_like(gt_images)
+            noised_known_regions = torch.sqrt(alpha_prev) * gt_images + torch.sqrt(1 - alpha_prev) * known_noise
+            img = img * masks + noised_known_regions * gt_keep_mask
+    return img * masks + gt_images * (1 - masks)  # the script's final blend (:692-696)
+
+
+def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
@@ -327,17 +381,22 @@ def main():
                     help="N=1 only: also time this many steps in the reduced-precision f16 mode, reported separately "
                          "(the reference's .half() experiment, code/test_quant.py:390-409; 0 = skip)")
     ap.add_argument("--ddpm-steps", type=int, default=1000, help="--workload ddpm: diffusion steps T (linear)")
-    ap.add_argument("--workload", choices=["sample", "c4", "train", "ddpm"], default="sample",
+    ap.add_argument("--workload", choices=["sample", "c4", "train", "ddpm", "dropin"], default="sample",
                     help="sample: the headline DDIM-100 sampler, --batch images per GPU (default; configs[1]); c4: the "
                          "same loop over a fixed global batch of 512 sharded over the ranks (configs[3]); train: the "
-                         "training step (configs[4]); ddpm: DDPM-1000 at B=64 (configs[2])")
+                         "training step (configs[4]); ddpm: DDPM-1000 at B=64 (configs[2]); dropin: configs[1] through "
+                         "the reference script's own per-step loop over model() (the fused rate beside it)")
     ap.add_argument("--global-batch", type=int, default=None,
                     help="sample / c4: total images over all ranks, sharded contiguously (sizes differ by at most "
                          "one; default --batch x ranks, or 512 for c4)")
     ap.add_argument("--noise", choices=["device", "parity"], default="device",
                     help="device: per-rank GPU RNG (throughput); parity: full-batch device draws in reference order, "
-                         "sliced per rank (GPU-count-independent results)")
-    args = ap.parse_args()
+                         "sliced per rank, batch-invariant conv geometry (GPU-count-independent results)")
+    return ap
+
+
+def main():
+    args = build_parser().parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     if args.workload == "train":
@@ -368,7 +427,8 @@ def main():
     if B < 1:
         raise SystemExit(f"bench: global batch {G} leaves rank {rank} of {ws} without images")
 
-    model = DiffusionInpaintingModel(FULL, device=dev, precision=args.precision)
+    opts = model_options(args)
+    model = DiffusionInpaintingModel(FULL, device=dev, precision=args.precision, options=opts)
     model.load_state_dict(make_state_dict(FULL, seed=1))
     model.eval()
     diffusion = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="cosine")
@@ -384,12 +444,22 @@ def main():
     handle = model.handle(dev)
     L = _lib.lib()
 
-    def one_pass(i):
+    dropin = args.workload == "dropin"
+
+    def fused_pass(i):
         torch.manual_seed(42 + i if args.noise == "parity" else 42 + 1000 * rank + i)
         with torch.no_grad():
             y = sampler.inpainting_ddim_sample_loop(sampler.model_fn, shape, gt, mask, True, dev, False, args.eta)
             y = sampler.final_blend(y, gt, mask)
             return parallel.gather_images(y, G)
+
+    def dropin_pass(i):
+        torch.manual_seed(42 + 1000 * rank + i)
+        with torch.no_grad():
+            y = script_ddim_pass(model, diffusion.alphas_cumprod, shape, gt, mask, args.ddim_steps, args.eta, dev)
+            return parallel.gather_images(y, G)
+
+    one_pass = dropin_pass if dropin else fused_pass
 
     prof = not args.no_profile
     import ctypes
@@ -422,6 +492,7 @@ def main():
     parallel.barrier(dev)
     elapsed = parallel.max_over_ranks(time.perf_counter() - t0, dev)
     assert torch.isfinite(y).all()
+    model.guard_check()  # the lazy range guard of the drop-in loop's forwards (raises on a trip)
 
     roofline = None
     if prof:
@@ -481,7 +552,11 @@ def main():
         "noise": args.noise,
         "config": {"workload": ("C4: CelebA-HQ-shaped 256x256, global batch sharded over the ranks, DDIM-100 cosine "
                                 "T=1000 eta=0.75, all_gather of the outputs (BASELINE configs[3])" if c4 else
+                                "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1]) "
+                                "through the reference script's per-step loop over model() "
+                                "(code/test_inp_ddim_100.py:470-576, lazy range guard)" if dropin else
                                 "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1])"),
+                   "options": opts,
                    "global_batch": G, "batch_per_gpu": B if G % ws == 0 else f"{G // ws}-{-(-G // ws)}",
                    "unet_evals_per_image": n_evals,
                    "gflop_per_unet_eval_per_image": round(gflop_per_image(FULL), 2),
@@ -489,7 +564,18 @@ def main():
         "roofline": roofline,
         "cpu_baseline": None,
     }
-    extras = ws == 1 and not c4  # the other arithmetic modes are timed beside the headline at N = 1 only
+    if dropin:  # the fused loop of the same run, same inputs, for the gap
+        fused_pass(0)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            fused_pass(1 + i)
+        torch.cuda.synchronize(dev)
+        elf = parallel.max_over_ranks(time.perf_counter() - t1, dev)
+        res["fused"] = {"value": round(G * args.steps / elf, 4), "unit": "images/s",
+                        "ms_per_step": round(elf / args.steps * 1e3, 2),
+                        "dropin_over_fused": round(value / (G * args.steps / elf), 4)}
+    extras = ws == 1 and not c4 and not dropin  # the other arithmetic modes beside the headline, N = 1 only
     if extras and args.precision != "fp32" and args.fp32_exact_steps > 0:
         # the same workload in exact-fp32 mode, timed separately (same inputs, same clocked region)
         model.precision = "fp32"

@@ -98,6 +98,11 @@ int ifd_guard_read(ifd_handle* h, int* tripped, void* stream) {
   return h->model->guard_read((hipStream_t)stream, tripped);
 }
 
+int ifd_guard_copy_async(ifd_handle* h, unsigned* host_dst, void* stream) {
+  if (!h || !host_dst) { set_error("ifd_guard_copy_async: null argument"); return 2; }
+  return h->model->guard_copy_async((hipStream_t)stream, host_dst);
+}
+
 int ifd_set_option(ifd_handle* h, const char* key, int value) {
   if (!h || !key) { set_error("ifd_set_option: null argument"); return 2; }
   return h->model->set_option(key, value);

@@ -56,6 +56,14 @@
 #ifndef X3_STORE_AUX
 #define X3_STORE_AUX 2
 #endif
+// Deferred output stores (X3_DEFER = phases, 0 = off): a unit whose successor on the block has at least
+// X3_DEFER chunks before its residual prefetch leaves its outputs (+ bias + residual) in the residual
+// registers and issues the 64 stores per lane as side work of the successor's first X3_DEFER chunks, so
+// that the consumer's MFMA stream does not wait behind the chip-wide store burst at every unit end
+// (profiles/r05a: the epilogue is store-drain-bound, ~6k of the +7.5k cycles a unit transition costs).
+#ifndef X3_DEFER
+#define X3_DEFER 4
+#endif
 #ifndef X3_RES_AUX
 #define X3_RES_AUX 0
 #endif
@@ -515,6 +523,30 @@ struct ResSide {
   }
 };
 
+// A unit's deferred output stores as side work of the NEXT unit's MFMA stream (X3_DEFER phases, one per
+// chunk): phase PH issues stores [PH NS, PH NS + NS) of the 64 per lane, spread over the chunk's 27 MFMA
+// groups, from the registers the values were left in (the residual-prefetch set, free until the unit's
+// last two chunks). Same addresses and layout as the immediate epilogue's stores.
+template <int TW, int NS, int PH>
+struct StoreSide {
+  const float (&xv)[2][2][16];
+  rsrc_t ro;
+  int vb[2];       // lane base per mr
+  int W4, cout4;   // output row width x cout x 4 B, cout x 4 B
+  template <int K>
+  __device__ __forceinline__ void step() const {
+    constexpr int lo = (K * NS + 26) / 27, hi = ((K + 1) * NS + 26) / 27;
+#pragma unroll
+    for (int i = PH * NS + lo; i < PH * NS + (hi < NS ? hi : NS); ++i) {
+      const int mr = i >> 5, nr = (i >> 4) & 1, r = i & 15;
+      const int lin = 8 * (r >> 2) + (r & 3);
+      const float x = xv[mr][nr][r];
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb[mr] + nr * 128,
+                                            ((lin / TW) * W4) + (lin % TW) * cout4, X3_STORE_AUX);
+    }
+  }
+};
+
 template <int XF, bool SKIP, int TW, int NPROD>
 __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
   using Geo = XGeo<TW>;
@@ -605,6 +637,71 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr) bias2[nr] = gld1(p.bias + t.ct * XBN + 32 * nr + l32);
     };
+    // GroupNorm granule statistics of the unit's outputs V(mr, nr, r) (the epilogue's values): over this
+    // lane's 32 pixels (two-pass), then merged with the other column half (lane ^ 32) and over the channel
+    // quad (lanes ^ 1, ^ 2). Every merge joins two equal counts, so Chan's update needs no division:
+    //   mean = ma + d / 2,  M2 = (M2a + M2b) + d^2 n / 2,  d = mb - ma  (n = one side's count)
+    // (bit-identical to gmerge: the factors are powers of two). The partner values come from
+    // v_permlane32_swap and DPP quad permutes (VALU) instead of LDS-routed shuffles, and the two channel
+    // blocks' chains are interleaved.
+    auto gstats = [&](const STile& t, auto&& V) __attribute__((always_inline)) {
+      float mean[2], m2[2];
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr) {
+        float sm = 0.f;
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sm += V(mr, nr, r);
+        mean[nr] = sm * (1.0f / 32);
+        float q = 0.f;
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float d = V(mr, nr, r) - mean[nr];
+            q += d * d;
+          }
+        m2[nr] = q;
+      }
+      auto merge = [&](float am, float aq, float bm, float bq, float n, float& om, float& oq) {
+        const float d = bm - am;
+        om = am + d * 0.5f;
+        oq = (aq + bq) + ((d * d) * n) * 0.5f;
+      };
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr) {  // lane ^ 32
+        float ml, mh, ql, qh;
+        wave_halves(mean[nr], ml, mh);
+        wave_halves(m2[nr], ql, qh);
+        merge(ml, ql, mh, qh, 32.f, mean[nr], m2[nr]);
+      }
+      // lanes ^ 1 then ^ 2 within the quad: quad_perm [0,0,2,2] / [1,1,3,3], then [0,1,0,1] / [2,3,2,3]
+#define IFD_QP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false))
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr)
+        merge(IFD_QP(mean[nr], 0xA0), IFD_QP(m2[nr], 0xA0), IFD_QP(mean[nr], 0xF5), IFD_QP(m2[nr], 0xF5), 64.f, mean[nr],
+              m2[nr]);
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr)
+        merge(IFD_QP(mean[nr], 0x44), IFD_QP(m2[nr], 0x44), IFD_QP(mean[nr], 0xEE), IFD_QP(m2[nr], 0xEE), 128.f, mean[nr],
+              m2[nr]);
+#undef IFD_QP
+      // through a buffer descriptor (scalar base, lane offset from a fresh lane id): a 64-bit per-lane
+      // pointer here was spilled, and its reload's vmcnt(0) waited for the unit's 64 output stores
+      const int ln = lane_id();
+      if (ln < 32 && (ln & 3) == 0) {
+        const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
+        const rsrc_t rg = mkrsrc(p.gstat + (size_t)(t.n0 + wimg) * (p.cout / 4) * p.gstat_E * 2);
+        const int vo = (ln >> 2) * p.gstat_E * 8;
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr) {
+          const int so = ((t.ct * 16 + nr * 8) * p.gstat_E + e) * 8;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mean[nr]), rg, vo, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m2[nr]), rg, vo + 4, so, 0);
+        }
+      }
+    };
     auto epilogue = [&](const STile& t, int z, const float (&rv)[2][2][16], bool tstamp = false) {
       if (X3_ABLATE == 13) {  // timing only: no epilogue
         asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][1]), "v"(acc[1][0]), "v"(acc[1][1]));
@@ -642,73 +739,36 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           }
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
         p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values + stores issued
-      if (X3_ABLATE != 15 && p.gstat) {
-        // GroupNorm granule statistics of each output channel: over this lane's 32 pixels (two-pass),
-        // then merged with the other column half (lane ^ 32) and over the channel quad (lanes ^ 1,
-        // ^ 2). Every merge joins two equal counts, so Chan's update needs no division:
-        //   mean = ma + d / 2,  M2 = (M2a + M2b) + d^2 n / 2,  d = mb - ma  (n = one side's count)
-        // (bit-identical to gmerge: the factors are powers of two). The partner values come from
-        // v_permlane32_swap and DPP quad permutes (VALU) instead of LDS-routed shuffles, and the two
-        // channel blocks' chains are interleaved.
-        float mean[2], m2[2];
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr) {
-          float sm = 0.f;
-#pragma unroll
-          for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) sm += acc[mr][nr][r];
-          mean[nr] = sm * (1.0f / 32);
-          float q = 0.f;
-#pragma unroll
-          for (int mr = 0; mr < 2; ++mr)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float d = acc[mr][nr][r] - mean[nr];
-              q += d * d;
-            }
-          m2[nr] = q;
-        }
-        auto merge = [&](float am, float aq, float bm, float bq, float n, float& om, float& oq) {
-          const float d = bm - am;
-          om = am + d * 0.5f;
-          oq = (aq + bq) + ((d * d) * n) * 0.5f;
-        };
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr) {  // lane ^ 32
-          float ml, mh, ql, qh;
-          wave_halves(mean[nr], ml, mh);
-          wave_halves(m2[nr], ql, qh);
-          merge(ml, ql, mh, qh, 32.f, mean[nr], m2[nr]);
-        }
-        // lanes ^ 1 then ^ 2 within the quad: quad_perm [0,0,2,2] / [1,1,3,3], then [0,1,0,1] / [2,3,2,3]
-#define IFD_QP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), ctrl, 0xf, 0xf, false))
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr)
-          merge(IFD_QP(mean[nr], 0xA0), IFD_QP(m2[nr], 0xA0), IFD_QP(mean[nr], 0xF5), IFD_QP(m2[nr], 0xF5), 64.f, mean[nr],
-                m2[nr]);
-#pragma unroll
-        for (int nr = 0; nr < 2; ++nr)
-          merge(IFD_QP(mean[nr], 0x44), IFD_QP(m2[nr], 0x44), IFD_QP(mean[nr], 0xEE), IFD_QP(m2[nr], 0xEE), 128.f, mean[nr],
-                m2[nr]);
-#undef IFD_QP
-        // through a buffer descriptor (scalar base, lane offset from a fresh lane id): a 64-bit per-lane
-        // pointer here was spilled, and its reload's vmcnt(0) waited for the unit's 64 output stores
-        const int ln = lane_id();
-        if (ln < 32 && (ln & 3) == 0) {
-          const int e = Geo::IMG > 1 ? 0 : ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
-          const rsrc_t rg = mkrsrc(p.gstat + (size_t)(t.n0 + wimg) * (p.cout / 4) * p.gstat_E * 2);
-          const int vo = (ln >> 2) * p.gstat_E * 8;
-#pragma unroll
-          for (int nr = 0; nr < 2; ++nr) {
-            const int so = ((t.ct * 16 + nr * 8) * p.gstat_E + e) * 8;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mean[nr]), rg, vo, so, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m2[nr]), rg, vo + 4, so, 0);
-          }
-        }
-      }
+      if (X3_ABLATE != 15 && p.gstat) gstats(t, [&](int mr, int nr, int r) { return acc[mr][nr][r]; });
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
         p.trace[64 * blockIdx.x + 45] = __builtin_amdgcn_s_memtime();  // statistics done
+    };
+    // The deferred epilogue (X3_DEFER): the outputs go to the residual registers xv (which hold the residual
+    // when there is one: x_res + (conv + bias), torch's order), their statistics are taken now, and the 64
+    // stores per lane are left to the next unit's first chunks (StoreSide); pvb / pro keep their addresses.
+    bool pend = false;
+    STile pt;  // the pending unit's tile (uniform: its store addresses are re-derived per chunk, no VGPR
+               // lives from one unit into the next)
+    auto epilogue_defer = [&](const STile& t, float (&xv)[2][2][16], bool tstamp = false) {
+      const bool hres = !SKIP && p.res;
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float x = acc[mr][nr][r] * (1.0f / kLo);  // exact rescale
+            x = x + bias2[nr];
+            if (hres) x = xv[mr][nr][r] + x;
+            xv[mr][nr][r] = x;
+          }
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
+        p.trace[64 * blockIdx.x + 44] = __builtin_amdgcn_s_memtime();  // values
+      if (X3_ABLATE != 15 && p.gstat) gstats(t, [&](int mr, int nr, int r) { return xv[mr][nr][r]; });
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && tstamp)
+        p.trace[64 * blockIdx.x + 45] = __builtin_amdgcn_s_memtime();  // statistics done
+      pt = t;
+      pend = true;
     };
     // ---- 1x1 skip chunks: the lane's operand = channels [XSK/2 h, XSK/2 (h + 1)) of the chunk at tile
     // pixels wm0 + 32 mr + l32, loaded into registers two chunks ahead. Sub-chunk q (one k = 16 MFMA
@@ -872,7 +932,27 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         // residual, or acc + fragments + the residual.
         const bool rpf = !SKIP && S == 1 && p.res;
         zero_l();
-        for (int c = c0; c < me - 2; ++c) main_chunk(true);
+        int c = c0;
+        if constexpr (X3_DEFER > 0 && !SKIP) {
+          if (pend) {  // the previous unit's 64 stores per lane, over this unit's first X3_DEFER chunks
+            constexpr int NS = 64 / (X3_DEFER > 0 ? X3_DEFER : 1);
+            const int W4 = p.W * p.cout * 4, c4 = p.cout * 4;
+            auto ss = [&](auto ph) __attribute__((always_inline)) {
+              const int vb0 = vbase(pt);
+              main_chunk_side(true, StoreSide<TW, NS, decltype(ph)::value>{
+                                        xr, mkrsrc(p.out + (size_t)pt.n0 * p.H * p.W * p.cout), {vb0, vb0 + mstep}, W4, c4});
+            };
+            ss(std::integral_constant<int, 0>{});
+            if constexpr (X3_DEFER > 1) ss(std::integral_constant<int, 1>{});
+            if constexpr (X3_DEFER > 2) {
+              ss(std::integral_constant<int, 2>{});
+              ss(std::integral_constant<int, 3>{});
+            }
+            c += X3_DEFER;
+            pend = false;
+          }
+        }
+        for (; c < me - 2; ++c) main_chunk(true);
         if (me > c0) {
           // the lane's id re-read here (volatile: not hoisted, so no per-lane address lives through the
           // whole unit loop for these loads: such values were spilled, and the reload's vmcnt(0) waited
@@ -946,11 +1026,13 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       if (SKIP && S == 1) bias_load(t);  // (SKIP kernels have no residual)
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
         p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
-      epilogue(t, z, xr, u == 0);
-      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0) {
-        __builtin_amdgcn_s_waitcnt(0);  // (trace builds: wait for the stores to leave)
-        p.trace[64 * blockIdx.x + 63] = __builtin_amdgcn_s_memtime();    // first epilogue: end
-      }
+      // deferred when the block's next unit has X3_DEFER chunks ahead of its residual prefetch to carry the stores
+      if (X3_DEFER > 0 && !SKIP && S == 1 && nmain - 2 >= X3_DEFER && u + 1 < nu)
+        epilogue_defer(t, xr, u == 0);
+      else
+        epilogue(t, z, xr, u == 0);
+      if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
+        p.trace[64 * blockIdx.x + 63] = __builtin_amdgcn_s_memtime();  // first epilogue: end (no store drain wait)
     }
     if (SKIP && p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
     if (IFD_TRACE && p.trace && wave == 0 && lane == 0) {  // consumer done (stores issued)

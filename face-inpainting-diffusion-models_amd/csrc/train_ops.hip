@@ -77,7 +77,7 @@ struct WgArgs {
   int64_t P;           // N * H * W
   int chunks_per_split;
   float* part;         // [S][cout][cin][taps]
-  // wgrad_x3_kernel<.., GNA = true>: X = silu(actA[n][c] x + actB[n][c]) of the raw x0, zero padded after the
+  // wgrad_ws_kernel<.., GNA = true>: X = silu(actA[n][c] x + actB[n][c]) of the raw x0, zero padded after the
   // activation (the forward conv's GroupNorm + SiLU prologue, recomputed at staging instead of materialised)
   const float* actA; const float* actB;
 };
@@ -378,34 +378,30 @@ __device__ __forceinline__ wx_h4 wx_tr(const _Float16* L, int off) {
   return __builtin_bit_cast(wx_h4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) wx_hv4*)(L + off)));
 }
 
-// Threads per block: the 3x3 kernel runs 8 waves, two per SIMD - waves w and w + 4 own the same 32 x 32
-// quadrant, taps 0-4 and 5-8 (80 / 64 accumulator registers instead of 144), so while one waits on an LDS
-// read or its staging the other's MFMAs run (round 2: one wave per SIMD with all 9 taps, ~45 % of its
-// MFMA-bound time); the 1x1 kernel keeps 4 waves.
+// Threads per block of the 1x1 kernel: 4 waves, one 32 x 32 quadrant of the 64 co x 64 ci tile each.
 template <int TAPS>
 struct WxCfg {
-  static constexpr int NT = TAPS == 9 ? 512 : 256;
+  static_assert(TAPS == 1, "wgrad_x3_kernel is the 1x1 weight gradient (3x3: wgrad_ws_kernel)");
+  static constexpr int NT = 256;
   static constexpr int DI = WX_PX * 16 / NT;                   // dY 16-B items per thread
-  static constexpr int XI = (WX_HMAX * 16 + NT - 1) / NT;      // X halo items per thread
-  static constexpr int NG = TAPS == 9 ? 2 : 1;                 // tap groups
-  static constexpr int NTMAX = TAPS == 9 ? 5 : 1;              // accumulators per wave
+  static constexpr int XI = (WX_HMAX * 16 + NT - 1) / NT;      // X items per thread
+  static constexpr int NTMAX = 1;                              // accumulators per wave
 };
 
 // colpart (optional): the bias gradient's column sums of dY, fused: the ci-tile-0 blocks add their
 // split's pixels per channel (fixed order: per thread over chunks, then the pixel lanes in lane
 // order) into colpart[split][cout]; colsum_final_kernel adds the splits in order.
-// TAPS = 9 (3x3, halo of one pixel) or 1 (1x1: the chunk's own pixels, no halo).
 // NPROD = 3 (fp32-class: three split products) or 1 (the reduced-precision f16 training mode: the hi x hi
 // product only; no lo planes are staged or read).
-// GNA: the X operand is the GroupNorm-applied, SiLU-activated raw input (WgArgs::actA / actB), computed
-// per staged value exactly as conv_x3.hip's producers compute it for the forward conv.
-// Launched for the 1x1 weight gradients; the 3x3 ones run wgrad_ws_kernel (below), whose consumer waves
-// carry no staging (this kernel's TAPS = 9 form measured 1.98 vs 1.79 ms, profiles/r04b/wgrad_exp).
-template <int TAPS, int NPROD, bool GNA>
-__global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
+// The 1x1 weight gradients (skip connections, qkv, proj_out): X = the chunk's own pixels, no halo. The 3x3
+// ones run wgrad_ws_kernel (below), whose consumer waves carry no staging (a 3x3 form of this kernel, every
+// wave staging beside its MFMAs, measured 1.98 vs 1.79 ms, profiles/r04b/wgrad_exp; removed in round 5).
+template <int NPROD>
+__global__ __launch_bounds__(WxCfg<1>::NT, 1) void wgrad_x3_kernel(WgArgs a, unsigned* guard, float* colpart) {
+  constexpr int TAPS = 1;
   using Cf = WxCfg<TAPS>;
   constexpr int NT = Cf::NT, WX_DI = Cf::DI, WX_XI = Cf::XI, NTMAX = Cf::NTMAX;
-  constexpr int HALO = TAPS == 9 ? 1 : 0;
+  constexpr int HALO = 0;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
   f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop (its last barrier)
   const int cin = a.c0 + a.c1;  // (X = concat(x0[c0], x1[c1]): a 64-channel tile never straddles them)
@@ -426,7 +422,7 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
   const int xst = src1 ? a.c1 : a.c0, xc0 = src1 ? ci0 - a.c0 : ci0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5;
-  const int quad = wave & 3, grp = Cf::NG > 1 ? wave >> 2 : 0;  // quadrant; tap group (taps 0-4 / 5-8)
+  const int quad = wave & 3;  // quadrant
   const int wr = 32 * (quad & 1), wc = 32 * (quad >> 1);
   const int Wc = a.W < 32 ? a.W : 32, R = WX_PX / Wc;
   const int HWc = Wc + 2 * HALO, HP = (R + 2 * HALO) * HWc;
@@ -449,8 +445,6 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
     const bool co_ok = co0 + 4 * cq + 3 < a.cout, ci_ok = ci0 + 4 * cq + 3 < cin;
     // two register sets (chunk parity): a chunk's loads go out two chunks before its staging
     f32x4 dvs[2][WX_DI], xvs[2][WX_XI];
-    f32x4 gas[GNA ? 2 : 1], gbs[GNA ? 2 : 1];  // GNA: the chunk's image's coefficients of the thread's quad
-    unsigned okm[GNA ? 2 : 1];                 // GNA: bit k = halo item k inside the map (else padding)
     int xhy[WX_XI], xhx[WX_XI], ld_x[WX_XI], ld_d[WX_DI];
 #pragma unroll
     for (int k = 0; k < WX_XI; ++k) {
@@ -487,20 +481,11 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       const int ox = __builtin_amdgcn_readfirstlane((y0 * a.W + x0) * xst * 4);
 #pragma unroll
       for (int k = 0; k < WX_DI; ++k) dv[k] = bld4(rd, co_ok ? ld_d[k] + od : WX_OOB, 0);
-      unsigned m = 0;
 #pragma unroll
       for (int k = 0; k < WX_XI; ++k) {
         const int y = y0 + xhy[k], x = x0 + xhx[k];
         const bool ok = ci_ok & ((unsigned)y < (unsigned)a.H) & ((unsigned)x < (unsigned)a.W);  // (no branches)
         xv[k] = bld4(rx, ok ? ld_x[k] + ox : WX_OOB, 0);
-        m |= ok ? 1u << k : 0u;
-      }
-      if constexpr (GNA) {
-        constexpr int S = decltype(SETc)::value;
-        okm[S] = m;
-        const int oc = ci_ok ? (ci0 + 4 * cq) * 4 : WX_OOB;
-        gas[S] = bld4(mkrsrc(a.actA + (size_t)n * cin), oc, 0);
-        gbs[S] = bld4(mkrsrc(a.actB + (size_t)n * cin), oc, 0);
       }
     };
     // staging of one chunk in WX_PARTS slices (items: the WX_DI dY quads, then the WX_XI halo quads), so
@@ -514,20 +499,9 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
         if (it >= WX_ITEMS) return;
         const bool isd = it < WX_DI;
         const int k = isd ? it : it - WX_DI;
-        f32x4 v = isd ? dv[k] : xv[k];
+        const f32x4 v = isd ? dv[k] : xv[k];
         const int row = (tid + NT * k) >> 4;
         if (!isd && row >= HP) return;
-        if constexpr (GNA) {
-          if (!isd) {  // conv_x3.hip's prologue: padding rides in the exponent (2^+inf -> rcp -> 0)
-            constexpr int S = decltype(SETc)::value;
-            const float pinf = (okm[S] >> k) & 1u ? 0.f : __builtin_inff();
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float t = fmaf(gas[S][j], v[j], gbs[S][j]);
-              v[j] = t * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(fmaf(t, -1.4426950408889634f, pinf)));
-            }
-          }
-        }
         if (isd && do_cs) csum += v;
         unsigned h0, l0, h1, l1;
         wx_split2(v[0], v[1], h0, l0);
@@ -590,8 +564,8 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       auto fetchB = [&](int st, int t, wx_h8& bhi, wx_h8& blo) {
         const int m0 = 16 * st;  // (wave-uniform part of the k-step's first pixel)
         const int hb = Wc >= 16 ? (m0 >> lwc) * HWc + (m0 & (Wc - 1)) : 2 * st * HWc;
-        const int r0 = TAPS == 9 ? hb + (t / 3) * HWc + (t % 3) : hb;
-        const _Float16* b = pB + __builtin_amdgcn_readfirstlane(r0 * WX_P);
+        (void)t;
+        const _Float16* b = pB + __builtin_amdgcn_readfirstlane(hb * WX_P);
         const wx_h4 bh0 = wx_tr(b, 0), bh1 = wx_tr(b, 4 * WX_P);
         bhi = wx_h8{bh0[0], bh0[1], bh0[2], bh0[3], bh1[0], bh1[1], bh1[2], bh1[3]};
         if (NPROD == 3) {
@@ -671,13 +645,8 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       _Float16* L = lds[c & 1];
       _Float16* Ln = lds[(c + 1) & 1];
       const bool nxt = c + 1 < c_end;
-      if (c < c_end) {  // (block-uniform; the dummy half of an odd count only loads)
-        if (TAPS == 9 && grp == 1)
-          mfma_chunk(std::integral_constant<int, 5>(), std::integral_constant<int, 4>(), L, Ln, nxt, SETc);
-        else
-          mfma_chunk(std::integral_constant<int, 0>(), std::integral_constant<int, TAPS == 9 ? 5 : 1>(), L, Ln, nxt,
-                     SETc);
-      }
+      if (c < c_end)  // (block-uniform; the dummy half of an odd count only loads)
+        mfma_chunk(std::integral_constant<int, 0>(), std::integral_constant<int, 1>(), L, Ln, nxt, SETc);
       load(clampc(c + 3), SETc);
       __syncthreads();
     };
@@ -702,18 +671,13 @@ __global__ __launch_bounds__(WxCfg<TAPS>::NT, 1) void wgrad_x3_kernel(WgArgs a, 
       }
     }
   }
-  // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin][TAPS]
-  float* slab = a.part + (size_t)zs * a.cout * cin * TAPS;
+  // C[i][j], i = 8 (r >> 2) + 4 h + (r & 3) (co), j = l32 (ci); slab [z][cout][cin]
+  float* slab = a.part + (size_t)zs * a.cout * cin;
   const int ci = ci0 + wc + (lane & 31);
-  const int tbase = TAPS == 9 ? 5 * grp : 0, ntap = TAPS == 9 ? (grp ? 4 : 5) : 1;
 #pragma unroll
-  for (int lt = 0; lt < NTMAX; ++lt) {
-    if (lt >= ntap) continue;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = co0 + wr + 8 * (r >> 2) + 4 * h + (r & 3);
-      if (co < a.cout && ci < cin) slab[((size_t)co * cin + ci) * TAPS + tbase + lt] = acc[lt][r];
-    }
+  for (int r = 0; r < 16; ++r) {
+    const int co = co0 + wr + 8 * (r >> 2) + 4 * h + (r & 3);
+    if (co < a.cout && ci < cin) slab[(size_t)co * cin + ci] = acc[0][r];
   }
 }
 
@@ -2426,10 +2390,9 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
   const bool fused_db = db && colpart && (int64_t)S * cout <= colpart_floats && cout % 4 == 0;
   float* cp = fused_db ? colpart : nullptr;
   const bool gna = actA != nullptr;
-  const dim3 g9(tiles, S), b9(WxCfg<9>::NT), b1(WxCfg<1>::NT);
+  const dim3 g9(tiles, S), b1(WxCfg<1>::NT);
   // 3x3: the warp-specialised kernel (wgrad_x3_kernel<9, ..> measured 1.98 vs 1.79 ms at 256^2 128 -> 128,
   // profiles/r04b/wgrad_exp); 1x1: wgrad_x3_kernel<1, ..>
-  (void)b9;
   if (taps == 9) {
     if (nprod == 3 && gna)
       hipLaunchKernelGGL((wgrad_ws_kernel<3, true>), g9, dim3(512), 0, s, a, guard, cp);
@@ -2440,9 +2403,9 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
     else
       hipLaunchKernelGGL((wgrad_ws_kernel<1, false>), g9, dim3(512), 0, s, a, guard, cp);
   } else if (nprod == 3)
-    hipLaunchKernelGGL((wgrad_x3_kernel<1, 3, false>), g9, b1, 0, s, a, guard, cp);
+    hipLaunchKernelGGL((wgrad_x3_kernel<3>), g9, b1, 0, s, a, guard, cp);
   else
-    hipLaunchKernelGGL((wgrad_x3_kernel<1, 1, false>), g9, b1, 0, s, a, guard, cp);
+    hipLaunchKernelGGL((wgrad_x3_kernel<1>), g9, b1, 0, s, a, guard, cp);
   const int64_t n = (int64_t)cout * cin * taps;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (fused_db) {

@@ -185,6 +185,7 @@ class Model {
   // range guard: async reset / synchronous read (0 = every split operand was in range)
   int guard_reset(hipStream_t s);
   int guard_read(hipStream_t s, int* tripped);
+  int guard_copy_async(hipStream_t s, unsigned* host_dst);
 };
 
 }  // namespace ifd

@@ -452,6 +452,15 @@ int Model::guard_read(hipStream_t s, int* tripped) {
   return 0;
 }
 
+int Model::guard_copy_async(hipStream_t s, unsigned* host_dst) {
+  if (!guard_) {
+    IFD_CHECK_HIP(hipMalloc(&guard_, 64));
+    IFD_CHECK_HIP(hipMemset(guard_, 0, 64));
+  }
+  IFD_CHECK_HIP(hipMemcpyAsync(host_dst, guard_, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  return 0;
+}
+
 int Model::set_precision(int prec) {
   IFD_REQUIRE(prec == IFD_PREC_FP32 || prec == IFD_PREC_3XF16 || prec == IFD_PREC_F16, "unknown precision mode");
   prec_ = prec;

@@ -64,6 +64,7 @@ EXPORTS = {
     "ifd_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     "ifd_guard_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ifd_guard_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]),
+    "ifd_guard_copy_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "ifd_get_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     "ifd_set_precision": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ifd_get_precision": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),

@@ -11,12 +11,21 @@ handed to the library (`ifd_load_weights`), which packs its own NHWC/KRSC-style 
 There is no CPU/PyTorch fallback: a CPU tensor or a missing library raises.
 
 precision="3xf16" is guarded: the split kernels flag any operand that reaches the f16 range
-(include/ifd.h ifd_guard_*); a flagged forward is recomputed in exact fp32 (counted in
-`guard_trips`), so the result is fp32-class for any input, not only for well-scaled weights.
+(include/ifd.h ifd_guard_*). Two ways to act on the flag (`guard=`, env IFD_GUARD):
+* "lazy" (the default): a forward never waits on the GPU. Each 3xf16 forward enqueues an asynchronous
+  copy of the (sticky) guard word into page-locked memory; the next forwards look at the copies whose
+  work has finished. A trip raises RuntimeError from a LATER forward (or from `guard_check()`), at most
+  a few forwards after the one that tripped; the outputs of the forwards in between are not recomputed —
+  the caller re-runs its loop, e.g. with precision="fp32". This is what a reference script's own loop
+  (model() once per step, code/test_inp_ddim_100.py:512-574) runs into, at no per-step cost.
+* "sync": each forward checks the guard after its launch (one stream synchronisation) and recomputes a
+  flagged forward in exact fp32 (counted in `guard_trips`): fp32-class for any input.
+The fused sampler loops (ifd.sampler) check once per loop and re-run the whole loop in fp32, in both.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -79,9 +88,12 @@ class Handle:
 class DiffusionInpaintingModel(torch.nn.Module):
     """9-channel inpainting UNet (code/unet.py:176-200) executed by libifd."""
 
-    def __init__(self, cfg: UNetConfig = FULL, device=None, precision: str = "3xf16", options=None):
+    def __init__(self, cfg: UNetConfig = FULL, device=None, precision: str = "3xf16", options=None, guard=None):
         super().__init__()
         self.cfg = cfg
+        self.guard = guard or os.environ.get("IFD_GUARD", "lazy")  # module docstring
+        if self.guard not in ("lazy", "sync"):
+            raise ValueError("guard must be 'lazy' or 'sync'")
         # handle options (include/ifd.h ifd_set_option), e.g. {"batch_invariant": 1}
         self.options = dict(options or {})
         if precision not in _lib.PRECISIONS:
@@ -105,6 +117,7 @@ class DiffusionInpaintingModel(torch.nn.Module):
         self.guard_trips = 0  # 3xf16 evals / loops recomputed in fp32 by the range guard
         self._applied = None  # (handle, precision, options) last pushed to the library
         self._deferred = None  # deferred_guard(): per-forward guard reads suspended
+        self._lz = None  # lazy guard: [handle id, pinned slots, pending [(event, slot)], next slot, armed]
 
     # -- weights -------------------------------------------------------------------------------
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
@@ -172,9 +185,65 @@ class DiffusionInpaintingModel(torch.nn.Module):
         out = torch.empty(B, self.cfg.out_channels, H, W, device=dev, dtype=torch.float32)
         h = self.handle(dev)
         L = _lib.lib()
-        self.run_guarded(h, dev, lambda: _lib.check(L.ifd_unet_forward(
-            h.h, _lib.ptr(xx), _lib.ptr(mi), _lib.ptr(mk), _lib.ptr(tt), B, H, W, _lib.ptr(out), _lib.stream_ptr(dev))))
+        launch = lambda: _lib.check(L.ifd_unet_forward(  # noqa: E731
+            h.h, _lib.ptr(xx), _lib.ptr(mi), _lib.ptr(mk), _lib.ptr(tt), B, H, W, _lib.ptr(out), _lib.stream_ptr(dev)))
+        if self.guard == "lazy" and self.precision != "fp32" and self._deferred is None:
+            self._lazy_forward(h, dev, launch)
+        else:
+            self.run_guarded(h, dev, launch)
         return out
+
+    # -- the lazy range guard (module docstring) -------------------------------------------------
+    _LZ_SLOTS = 8
+
+    def _lazy_forward(self, h, dev, launch):
+        L = _lib.lib()
+        s = _lib.stream_ptr(dev)
+        if self._lz is None or self._lz[0] != id(h):
+            self._lz = [id(h), torch.zeros(self._LZ_SLOTS, dtype=torch.int32, pin_memory=True), [], 0, False]
+        lz = self._lz
+        self._lazy_poll(block=len(lz[2]) >= self._LZ_SLOTS)  # a full ring waits for its oldest copy
+        if not lz[4]:  # armed once: the word is sticky, so one reset covers every later forward
+            _lib.check(L.ifd_guard_reset(h.h, s))
+            lz[4] = True
+        launch()
+        slot = lz[3]
+        lz[3] = (slot + 1) % self._LZ_SLOTS
+        _lib.check(L.ifd_guard_copy_async(h.h, ctypes.c_void_p(lz[1][slot:].data_ptr()), s))
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        lz[2].append((ev, slot))
+
+    def _lazy_poll(self, block=False):
+        """Look at the guard copies whose work has finished (all of them with block=True; the oldest one
+        when the ring is full); raise on a trip."""
+        lz = self._lz
+        if lz is None:
+            return
+        pend = lz[2]
+        while pend:
+            ev, slot = pend[0]
+            if block:
+                ev.synchronize()
+            elif not ev.query():
+                break
+            pend.pop(0)
+            if int(lz[1][slot]):
+                pend.clear()
+                lz[4] = False  # re-armed (reset) by the next lazy forward
+                self.guard_trips += 1
+                raise RuntimeError("ifd: 3xf16 range guard tripped (a conv operand reached the f16 range) in an "
+                                   "earlier forward; its output and the later ones are not fp32-accurate: re-run "
+                                   "with precision='fp32' (or guard='sync', which recomputes each flagged forward)")
+            block = False
+
+    def guard_check(self):
+        """Wait for every lazy guard copy and raise if any forward since the last check tripped."""
+        lz = self._lz
+        if lz is None:
+            return
+        while lz[2]:
+            self._lazy_poll(block=True)
 
     def deferred_guard(self):
         """Context manager for a caller-driven loop of 3xf16 forwards (e.g. a reference script's own
@@ -193,7 +262,12 @@ class DiffusionInpaintingModel(torch.nn.Module):
             h = self.handle(dev)
             L = _lib.lib()
             s = _lib.stream_ptr(dev)
+            self.guard_check()  # a lazy trip not yet seen is reported, not cleared by the reset
             _lib.check(L.ifd_guard_reset(h.h, s))
+            # the scope's forwards may run on other streams: the reset (ordered on `s` only) lands first
+            torch.cuda.synchronize(dev)
+            if self._lz is not None:
+                self._lz[4] = False
             self._deferred = dev
             try:
                 yield
@@ -217,7 +291,10 @@ class DiffusionInpaintingModel(torch.nn.Module):
             return launch()
         L = _lib.lib()
         s = _lib.stream_ptr(dev)
+        self.guard_check()  # a lazy trip not yet seen is reported, not cleared by the reset
         _lib.check(L.ifd_guard_reset(h.h, s))
+        if self._lz is not None:
+            self._lz[4] = False
         res = launch()
         tripped = ctypes.c_int()
         _lib.check(L.ifd_guard_read(h.h, ctypes.byref(tripped), s))

@@ -440,7 +440,9 @@ class UNetTrainer:
         stats = self._empty(N * 64)
         g = self._granules2(x, x1) if x1 is not None else self._gstat.get(x.data_ptr())
         if x1 is not None:
-            assert g is not None and C % 128 == 0, "a concat GroupNorm on load needs both sources' granules"
+            if g is None or C % 128 != 0:  # explicit (not an assert: `python -O` must not reach the wrong memory)
+                raise RuntimeError("ifd.train: a concat GroupNorm on load needs both sources' granule statistics "
+                                   "and C % 128 == 0")
             g = (x,) + g[1:]
         gam, bet = self.p(prefix + "weight"), self.p(prefix + "bias")
         if g is not None and g[0] is x and C % 128 == 0:

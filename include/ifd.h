@@ -92,6 +92,12 @@ int ifd_set_precision(ifd_handle* h, int prec);
  * IFD_PREC_FP32 (ifd.model / ifd.sampler do this automatically). */
 int ifd_guard_reset(ifd_handle* h, void* stream);
 int ifd_guard_read(ifd_handle* h, int* tripped, void* stream);
+/* The guard word, without a synchronisation: enqueues on `stream` a copy of the word into *host_dst
+ * (4 bytes; page-locked host memory, or the copy is not asynchronous) and returns. The value is valid
+ * once the work enqueued on `stream` before this call has finished (an event recorded after it).
+ * ifd.model's default "lazy" guard uses it so that a caller-driven loop of forwards (the reference
+ * scripts' model() per step) never waits on the GPU; see DiffusionInpaintingModel(guard=...). */
+int ifd_guard_copy_async(ifd_handle* h, unsigned* host_dst, void* stream);
 int ifd_get_precision(ifd_handle* h, int* prec);
 /* Handle options. No reference counterpart: execution choices of this library that never change
  * the arithmetic of a single image except where noted. Initial values are read from the

@@ -47,3 +47,49 @@ def test_pmc_traffic_picks_newest_summary(tmp_path, monkeypatch):
 def test_committed_pmc_summary_has_the_dominant_kernel():
     got = bench.pmc_traffic("conv_x3_kernel<0,false,32,3>")
     assert got["traffic"] and got["traffic"] > 1e8
+
+
+def test_parity_mode_requests_batch_invariant():
+    """`--noise parity` builds the model with the batch-invariant conv geometry: a
+    rank's shard is then bit-equal to the same images in any other batch, so the line is
+    GPU-count-independent; the default throughput mode keeps the fastest geometry."""
+    ap = bench.build_parser()
+    assert bench.model_options(ap.parse_args(["--noise", "parity"])) == {"batch_invariant": 1}
+    assert bench.model_options(ap.parse_args(["--noise", "parity", "--workload", "c4"])) == {"batch_invariant": 1}
+    assert bench.model_options(ap.parse_args([])) == {}
+
+
+def test_device_key_keeps_pci_ids_beside_uuid():
+    """Two devices whose ROCm build reports the same (e.g. all-zero) UUID still count as two."""
+    from types import SimpleNamespace
+    a = SimpleNamespace(uuid="00000000-0000-0000-0000-000000000000", pci_domain_id=0, pci_bus_id=0x15, pci_device_id=0)
+    b = SimpleNamespace(uuid="00000000-0000-0000-0000-000000000000", pci_domain_id=0, pci_bus_id=0x75, pci_device_id=0)
+    assert bench.device_key("n0", a) != bench.device_key("n0", b)
+    assert bench.device_key("n0", a) == bench.device_key("n0", SimpleNamespace(**vars(a)))
+    assert bench.device_key("n0", a) != bench.device_key("n1", a)
+
+
+def test_script_ddim_pass_is_the_reference_loop():
+    """bench's drop-in workload restates the reference script's loop (code/test_inp_ddim_100.py:470-576 +
+    the final blend :692-696) around model(): on CPU with a stand-in model it equals the oracle's
+    restatement of the same script (tests/golden pins that oracle bit-exact to the reference) bit for bit."""
+    from oracle import ref_diffusion
+    tb = ref_diffusion.Tables(ref_diffusion.get_named_beta_schedule("cosine", 1000))
+
+    def stub_unet(x, t, masked, m):  # deterministic, depends on every input
+        s = (t.to(torch.float32) / 1000.0).view(-1, 1, 1, 1)
+        eps = 0.3 * x + 0.2 * masked - 0.1 * m + s
+        return torch.cat([eps, 0.5 * eps], dim=1)
+
+    class Stub:
+        def __call__(self, x, t, masked_image=None, mask=None):
+            return stub_unet(x, t, masked_image, mask)
+
+    gt, mask = bench.synth_inputs(2, 32, seed=5, device="cpu")
+    shape = (2, 3, 32, 32)
+    torch.manual_seed(11)
+    a = bench.script_ddim_pass(Stub(), tb.ac, shape, gt, mask, 10, 0.75, "cpu")
+    torch.manual_seed(11)
+    b = ref_diffusion.final_blend(ref_diffusion.script_ddim_loop(tb, ref_diffusion.model_fn_factory(stub_unet), shape,
+                                                                 gt, mask, 10, clip=True, eta=0.75), gt, mask)
+    assert torch.equal(a, b)

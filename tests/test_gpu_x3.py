@@ -193,12 +193,12 @@ def _scaled_state_dict(layer="input_blocks.1.0.in_layers.0.", factor=1e5):
 
 
 def test_x3_range_guard_forward(evals, record):
-    """An out-of-f16-range operand trips the guard and the forward is recomputed in fp32: the
-    3xf16 model returns exactly the fp32 model's output (code/nn.py:184,212 feed the raw residual
+    """guard="sync": an out-of-f16-range operand trips the guard and the forward is recomputed in fp32:
+    the 3xf16 model returns exactly the fp32 model's output (code/nn.py:184,212 feed the raw residual
     stream to the 1x1 skip as well; both operand paths are guarded)."""
     from ifd.model import DiffusionInpaintingModel
     sd = _scaled_state_dict()
-    m3 = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16")
+    m3 = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16", guard="sync")
     m3.load_state_dict(sd)
     m32 = DiffusionInpaintingModel(FULL, device=DEV, precision="fp32")
     m32.load_state_dict(sd)
@@ -212,6 +212,31 @@ def test_x3_range_guard_forward(evals, record):
     assert m3.guard_trips == 1
     assert torch.equal(y3, y32)
     assert torch.isfinite(y3).all()
+
+
+def test_x3_range_guard_lazy(evals):
+    """guard="lazy" (the default): forwards never wait on the GPU; a trip is reported by a later forward
+    or by guard_check() as a RuntimeError (the flagged outputs are not recomputed), counted once, and the
+    guard is re-armed afterwards: in-range forwards of the same model then pass again."""
+    from ifd.model import DiffusionInpaintingModel
+    x, gt, mask = (_t(evals[f"full/{k}"]).to(DEV) for k in ("x", "gt", "mask"))
+    t = torch.tensor([500], device=DEV)
+    m3 = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16")
+    assert m3.guard == "lazy"
+    m3.load_state_dict(_scaled_state_dict())
+    with torch.no_grad():
+        m3(x, t, masked_image=gt * (1 - mask), mask=mask)  # trips; nothing waits here
+        with pytest.raises(RuntimeError, match="range guard tripped"):
+            for _ in range(3):  # raised by a later forward once the copy has landed, or by the check
+                m3(x, t, masked_image=gt * (1 - mask), mask=mask)
+            m3.guard_check()
+    assert m3.guard_trips == 1
+    m3.load_state_dict(make_state_dict(FULL, seed=1))
+    with torch.no_grad():
+        for _ in range(3):
+            m3(x, t, masked_image=gt * (1 - mask), mask=mask)
+        m3.guard_check()
+    assert m3.guard_trips == 1
 
 
 def test_x3_range_guard_quiet_on_manifest(evals, x3_model):
@@ -265,3 +290,11 @@ def test_x3_deferred_guard_scope(evals, x3_model):
         with m3.deferred_guard():
             m3(x, t, masked_image=gt * (1 - mask), mask=mask)
     assert m3.guard_trips == 1
+    # the scope's forwards on a second stream: the entry reset is ordered before them, so the trip is
+    # still seen at the exit
+    side = torch.cuda.Stream(DEV)
+    with torch.no_grad(), pytest.raises(RuntimeError, match="deferred_guard"):
+        with m3.deferred_guard():
+            with torch.cuda.stream(side):
+                m3(x, t, masked_image=gt * (1 - mask), mask=mask)
+    assert m3.guard_trips == 2

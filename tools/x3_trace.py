@@ -31,9 +31,12 @@ np.set_printoptions(linewidth=220)
 med = lambda a: np.median(a, axis=0).astype(int)
 print("interval (consumer start j -> j+1):", med(np.diff(cs, axis=1)))
 print("consumer issue (start -> MFMAs issued):", med(ce - cs))
-print("producer: interval start -> DMA+loads issued:", med(pi[:, 1:] - cs[:, 1:]))
-print("producer: loads issued -> LDS writes done:", med(ps - pi))
-print("producer: LDS writes done -> next consumer start:", med(cs[:, 1:] - ps[:, :-1]))
+# the producer stamps cover intervals 0..7 only (slots 32..39 and 48..55; 40..47 and 56..63 hold the fill
+# and the consumer's first-epilogue stamps). Producer interval j starts with the consumer's chunk j.
+pi, ps = pi[:, :8], ps[:, :8]
+print("producer: interval start -> LDS writes of the next chunk done (j = 0..7):", med(ps - cs[:, :8]))
+print("producer: interval start -> DMA + loads issued (j = 0..7):", med(pi - cs[:, :8]))
+print("producer: issued -> next interval start (its wait at the barrier):", med(cs[:, 1:9] - pi))
 print("first epilogue: start after chunk 0 start", int(np.median(blk[:, 43] - cs[:, 0])),
-      "; phases from its start (values + stores issued, statistics, stores drained):",
+      "; phases from its start (values [+ stores] issued, statistics [+ stores] issued, epilogue end):",
       [int(np.median(blk[:, k] - blk[:, 43])) for k in (44, 45, 63)])
