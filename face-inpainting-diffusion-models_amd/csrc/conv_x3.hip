@@ -64,6 +64,9 @@
 #ifndef X3_DEFER
 #define X3_DEFER 4
 #endif
+#ifndef X3_DEFER1_OFF  // (development A/B: 1 = no deferral for one-chunk units)
+#define X3_DEFER1_OFF 0
+#endif
 #ifndef X3_RES_AUX
 #define X3_RES_AUX 0
 #endif
@@ -934,7 +937,8 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         zero_l();
         int c = c0;
         if constexpr (X3_DEFER > 0 && !SKIP) {
-          if (pend) {  // the previous unit's 64 stores per lane, over this unit's first X3_DEFER chunks
+          if (pend && nmain - 2 >= X3_DEFER) {  // the previous unit's 64 stores per lane, over this unit's first
+                                                // X3_DEFER chunks (a one-chunk unit carries them below)
             constexpr int NS = 64 / (X3_DEFER > 0 ? X3_DEFER : 1);
             const int W4 = p.W * p.cout * 4, c4 = p.cout * 4;
             auto ss = [&](auto ph) __attribute__((always_inline)) {
@@ -984,10 +988,16 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
               main_chunk(false);
           } else {  // a one-chunk unit: all of the residual in its first third
             fold();
-            if (rpf)
+            if (rpf) {
               main_chunk_side(false, ResSide<TW, 0, 64, 9>{xr, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
-            else
+            } else if (X3_DEFER > 0 && !SKIP && pend) {  // (the 16 -> 128 input conv) the previous unit's
+              const int vp = vbase(pt);                    // stores, all 64 in this unit's one chunk
+              main_chunk_side(false, StoreSide<TW, 64, 0>{xr, mkrsrc(p.out + (size_t)pt.n0 * p.H * p.W * p.cout),
+                                                          {vp, vp + mstep}, W4, c4});
+              pend = false;
+            } else {
               main_chunk(false);
+            }
           }
         }
       } else {
@@ -1026,8 +1036,10 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       if (SKIP && S == 1) bias_load(t);  // (SKIP kernels have no residual)
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
         p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
-      // deferred when the block's next unit has X3_DEFER chunks ahead of its residual prefetch to carry the stores
-      if (X3_DEFER > 0 && !SKIP && S == 1 && nmain - 2 >= X3_DEFER && u + 1 < nu)
+      // deferred when the block's next unit has X3_DEFER chunks ahead of its residual prefetch to carry the stores,
+      // or is a single chunk without a residual (its chunk carries all 64)
+      if (X3_DEFER > 0 && !SKIP && S == 1 && u + 1 < nu &&
+          (nmain - 2 >= X3_DEFER || (!X3_DEFER1_OFF && nmain == 1 && !p.res)))
         epilogue_defer(t, xr, u == 0);
       else
         epilogue(t, z, xr, u == 0);

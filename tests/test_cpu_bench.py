@@ -93,3 +93,19 @@ def test_script_ddim_pass_is_the_reference_loop():
     b = ref_diffusion.final_blend(ref_diffusion.script_ddim_loop(tb, ref_diffusion.model_fn_factory(stub_unet), shape,
                                                                  gt, mask, 10, clip=True, eta=0.75), gt, mask)
     assert torch.equal(a, b)
+
+
+def test_fp32_accuracy_note_reads_newest_parity(tmp_path, monkeypatch):
+    """The fp32_exact entry states its measured accuracy against the reference: the ratio of
+    the mode's per-eval error vs fp64 to the reference's own, from the newest parity record that holds it."""
+    for tag, g in (("r01x", 4e-7), ("r02x", 2e-7)):
+        d = tmp_path / "profiles" / tag
+        d.mkdir(parents=True)
+        (d / "parity.json").write_text(json.dumps({"c1_eval0/fp32": {
+            "gpu_vs_fp64": {"mean": g, "p999": 2 * g, "max": 4 * g},
+            "reference_vs_fp64": {"mean": 1e-7, "p999": 2e-7, "max": 4e-7}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    note = bench.fp32_accuracy_note()
+    assert note["per_eval_error_vs_reference_own"] == {"mean": 2.0, "p999": 2.0, "max": 2.0}
+    assert note["source"].endswith("r02x/parity.json")
+    assert "NOT fp32-class" in note["note"]
