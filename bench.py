@@ -228,7 +228,8 @@ def train_main(args):
     sd = make_state_dict(FULL, seed=1)
 
     def run(precision, steps, warmup):
-        tr = UNetTrainer(FULL, device=dev, precision=precision, fuse_gn=os.environ.get("IFD_TRAIN_FUSE_GN", "1") != "0")
+        tr = UNetTrainer(FULL, device=dev, precision=precision, fuse_gn=os.environ.get("IFD_TRAIN_FUSE_GN", "1") != "0",
+                         fuse_gnb=os.environ.get("IFD_TRAIN_FUSE_GNB", "1") != "0")
         tr.load_state_dict(sd)
         gen = torch.Generator(device=dev).manual_seed(1 + rank)
 

@@ -92,6 +92,22 @@ struct ConvParams {
   int x3_nprod;
 };
 
+// Training (conv_x3's GNB instantiation, single-image tiles, no split-K, no residual): the conv's output is the
+// upstream gradient da of a GroupNorm(32) (+ scale/shift) (+ SiLU) whose input x = concat(x0[c0], x1) has `cout`
+// channels at the output's pixels; the epilogue also writes that GroupNorm backward's pass-1 partial sums
+// (train_ops.hip gn_bwd_partial_kernel's A1 = sum dz, A2 = sum dz nrm, A3 = sum dz (1 + s) xhat) per
+// (image, 64-pixel wave block e, channel): part[((n * nsl + e) * cout + c) * 3 + k]. A separate kernel
+// argument, so the sampler's instantiations keep their ConvParams-only signature (and register allocation).
+struct GnbParams {
+  const float* x0; const float* x1; int c0;
+  const float* stats;  // [N][32][2] (mean, rstd)
+  const float* gamma; const float* beta;
+  const float* ss; int ss_stride;  // optional scale [n][c], shift [n][cout + c]
+  int silu;
+  float* part; int nsl;
+};
+int launch_conv_x3_gnb(const ConvParams& p, const GnbParams& g, hipStream_t stream);
+
 // Launch with the tile configuration chosen from (cout, taps, xform). Returns hipError_t.
 int launch_conv(const ConvParams& p, int taps, int xform, int bn, hipStream_t stream);
 int conv_pick_bn(int cout, int taps, int H, int W, int N);

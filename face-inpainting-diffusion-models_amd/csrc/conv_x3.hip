@@ -550,8 +550,8 @@ struct StoreSide {
   }
 };
 
-template <int XF, bool SKIP, int TW, int NPROD>
-__global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
+template <int XF, bool SKIP, int TW, int NPROD, bool GNB>
+__device__ __forceinline__ void conv_x3_body(const ConvParams& p, const GnbParams& g) {
   using Geo = XGeo<TW>;
   extern __shared__ __attribute__((aligned(16))) float smem_raw[];
   lds_f* const smem = (lds_f*)(smem_raw);
@@ -773,6 +773,95 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
       pt = t;
       pend = true;
     };
+    // Training (ConvParams::gnb_*): this conv is the dgrad whose output da feeds a GroupNorm(+ scale/shift)(+ SiLU)
+    // backward; x (that GroupNorm's input, prefetched into xr like a residual) gives per value
+    //   xhat = (x - mean) rstd, nrm = xhat gamma + beta, z = nrm (1 + s) + sh, dz = da silu'(z) (or da),
+    // and the epilogue adds over the wave's 64 pixels, per channel, A1 = sum dz, A2 = sum dz nrm and
+    // A3 = (1 + s) sum dz xhat - gn_bwd_partial_kernel's pass 1 (train_ops.hip) without its pass over (da, x).
+    // The outputs are then stored as in the other epilogues (deferred from xr, or at once from acc).
+    auto epilogue_gnb = [&](const STile& t, float (&xv)[2][2][16], bool dfr) {
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float x = acc[mr][nr][r] * (1.0f / kLo);  // exact rescale
+            acc[mr][nr][r] = x + bias2[nr];
+          }
+      const int ln = lane_id(), ll = ln & 31;
+      const int n = t.n0 + wimg, C = p.cout, cpg = C / 32;
+      float a1[2], a2[2], a3[2], onep[2];
+#pragma unroll
+      for (int nr = 0; nr < 2; ++nr) {
+        const int cc = t.ct * XBN + 32 * nr + ll, grp = cc / cpg;
+        const float mean = g.stats[(n * 32 + grp) * 2], rstd = g.stats[(n * 32 + grp) * 2 + 1];
+        const float gam = g.gamma[cc], bet = g.beta[cc];
+        onep[nr] = g.ss ? 1.0f + g.ss[(size_t)n * g.ss_stride + cc] : 1.0f;
+        const float sh = g.ss ? g.ss[(size_t)n * g.ss_stride + C + cc] : 0.0f;
+        float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float xhat = (xv[mr][nr][r] - mean) * rstd;
+            const float nrm = xhat * gam + bet;
+            const float zz = nrm * onep[nr] + sh;
+            float dz = acc[mr][nr][r];
+            if (g.silu) {
+              const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zz * -1.4426950408889634f));
+              dz = dz * (sg * (1.0f + zz * (1.0f - sg)));
+            }
+            s1 += dz;
+            s2 += dz * nrm;
+            s3 += dz * xhat;
+            if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // (four values at a time: a short live set)
+          }
+        // + the other column half of the same pixel rows (lane ^ 32), same channel
+        float lo, hi;
+        wave_halves(s1, lo, hi);
+        a1[nr] = lo + hi;
+        wave_halves(s2, lo, hi);
+        a2[nr] = lo + hi;
+        wave_halves(s3, lo, hi);
+        a3[nr] = (lo + hi) * onep[nr];
+      }
+      if (ln < 32) {
+        const int e = ((t.y0 / p.TH) * p.tiles_x + t.x0 / p.TW) * 4 + wave;
+        float* o = g.part + ((size_t)n * g.nsl + e) * C * 3;
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr) {
+          const int cc = t.ct * XBN + 32 * nr + ll;
+          o[cc * 3] = a1[nr];
+          o[cc * 3 + 1] = a2[nr];
+          o[cc * 3 + 2] = a3[nr];
+        }
+      }
+      if (dfr) {  // the outputs into the residual registers: their stores go out during the next unit's chunks
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+          for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) xv[mr][nr][r] = acc[mr][nr][r];
+        pt = t;
+        pend = true;
+      } else {
+        const rsrc_t ro = mkrsrc(p.out + (size_t)t.n0 * p.H * p.W * p.cout);
+        const int vb = vbase(t);
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr)
+#pragma unroll
+          for (int mr = 0; mr < 2; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float x = acc[mr][nr][r];
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + mr * mstep + nr * 128,
+                                                    roff(r), X3_STORE_AUX);
+            }
+      }
+    };
     // ---- 1x1 skip chunks: the lane's operand = channels [XSK/2 h, XSK/2 (h + 1)) of the chunk at tile
     // pixels wm0 + 32 mr + l32, loaded into registers two chunks ahead. Sub-chunk q (one k = 16 MFMA
     // step) takes channels XSK/2 h + 8 q + (0..7), quads 2q and 2q+1; the host packs the weights in
@@ -933,7 +1022,10 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         // accumulates the corrections in accl), then the fold, then the mr = 1 half over the first third
         // of chunk me - 1 (its correction products go to acc). Peak: acc + accl + fragments + half the
         // residual, or acc + fragments + the residual.
-        const bool rpf = !SKIP && S == 1 && p.res;
+        // gnb (training): the last two chunks prefetch the GroupNorm input x instead of a residual (the host
+        // never sets both)
+        const bool gnb = GNB && !SKIP && S == 1 && g.part;
+        const bool rpf = !SKIP && S == 1 && (p.res || gnb);
         zero_l();
         int c = c0;
         if constexpr (X3_DEFER > 0 && !SKIP) {
@@ -971,25 +1063,35 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
           }
           const int up = p.res_xform != XF_NONE;
           const int cu = t.ct * XBN;
-          const int vn = (((wimg * p.H + t.y0 + wrow) * p.W + t.x0 + 4 * lh) * p.cout + cu + ll) * 4;
+          // the prefetched tensor's channels: the residual's (cout), or (GNB) the 64-channel tile's concat source
+          int Cx = p.cout, cux = cu;
+          const float* xsrc = p.res ? p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout : p.bias;
+          if constexpr (GNB) {
+            const bool xs1 = cu >= g.c0;
+            Cx = xs1 ? p.cout - g.c0 : g.c0;
+            cux = xs1 ? cu - g.c0 : cu;
+            xsrc = (xs1 ? g.x1 : g.x0) + (size_t)t.n0 * p.H * p.W * Cx;
+          }
+          const int vn = (((wimg * p.H + t.y0 + wrow) * p.W + t.x0 + 4 * lh) * Cx + cux + ll) * 4;
           const int vu = (2 * lh * p.cout + cu + ll) * 4;
-          const rsrc_t rr = mkrsrc(p.res ? p.res + (size_t)t.n0 * p.res_H * p.res_W * p.cout : p.bias);
-          const int vb0 = up ? vu : vn, vb1 = up ? vu : vn + mstep;
+          const rsrc_t rr = mkrsrc(xsrc);
+          const int vb0 = up ? vu : vn, vb1 = up ? vu : vn + (GNB ? (32 / TW) * p.W * Cx * 4 : mstep);
           const int W4 = p.W * p.cout * 4, c4 = p.cout * 4;
+          const int W4r = GNB ? p.W * Cx * 4 : W4, c4r = GNB ? Cx * 4 : c4;  // (residual / x strides)
           if (me - c0 >= 2) {
             if (rpf)
-              main_chunk_side(true, ResSide<TW, 0, 32, 27>{xr, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+              main_chunk_side(true, ResSide<TW, 0, 32, 27>{xr, rr, {vb0, vb1}, up, W4r, c4r, wm0, t.y0, t.x0, p.res_W});
             else
               main_chunk(true);
             fold();
             if (rpf)
-              main_chunk_side(false, ResSide<TW, 32, 64, 9>{xr, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+              main_chunk_side(false, ResSide<TW, 32, 64, 9>{xr, rr, {vb0, vb1}, up, W4r, c4r, wm0, t.y0, t.x0, p.res_W});
             else
               main_chunk(false);
           } else {  // a one-chunk unit: all of the residual in its first third
             fold();
             if (rpf) {
-              main_chunk_side(false, ResSide<TW, 0, 64, 9>{xr, rr, {vb0, vb1}, up, W4, c4, wm0, t.y0, t.x0, p.res_W});
+              main_chunk_side(false, ResSide<TW, 0, 64, 9>{xr, rr, {vb0, vb1}, up, W4r, c4r, wm0, t.y0, t.x0, p.res_W});
             } else if (X3_DEFER > 0 && !SKIP && pend) {  // (the 16 -> 128 input conv) the previous unit's
               const int vp = vbase(pt);                    // stores, all 64 in this unit's one chunk
               main_chunk_side(false, StoreSide<TW, 64, 0>{xr, mkrsrc(p.out + (size_t)pt.n0 * p.H * p.W * p.cout),
@@ -1038,11 +1140,18 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
         p.trace[64 * blockIdx.x + 43] = __builtin_amdgcn_s_memtime();  // first epilogue: start
       // deferred when the block's next unit has X3_DEFER chunks ahead of its residual prefetch to carry the stores,
       // or is a single chunk without a residual (its chunk carries all 64)
-      if (X3_DEFER > 0 && !SKIP && S == 1 && u + 1 < nu &&
-          (nmain - 2 >= X3_DEFER || (!X3_DEFER1_OFF && nmain == 1 && !p.res)))
-        epilogue_defer(t, xr, u == 0);
-      else
-        epilogue(t, z, xr, u == 0);
+      const bool gnbu = GNB && !SKIP && S == 1 && g.part;
+      const bool dfr = X3_DEFER > 0 && !SKIP && S == 1 && u + 1 < nu &&
+                       (nmain - 2 >= X3_DEFER || (!X3_DEFER1_OFF && nmain == 1 && !p.res && !gnbu));
+      if constexpr (GNB) {  // (launched only with gnb_part set and S == 1)
+        (void)gnbu;
+        epilogue_gnb(t, xr, dfr);
+      } else {
+        if (dfr)
+          epilogue_defer(t, xr, u == 0);
+        else
+          epilogue(t, z, xr, u == 0);
+      }
       if (IFD_TRACE && p.trace && wave == 0 && lane == 0 && u == 0)
         p.trace[64 * blockIdx.x + 63] = __builtin_amdgcn_s_memtime();  // first epilogue: end (no store drain wait)
     }
@@ -1151,6 +1260,15 @@ __global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
 }
 
 template <int XF, bool SKIP, int TW, int NPROD>
+__global__ __launch_bounds__(NT, 2) void conv_x3_kernel(ConvParams p) {
+  conv_x3_body<XF, SKIP, TW, NPROD, false>(p, GnbParams{});
+}
+template <int TW, int NPROD>
+__global__ __launch_bounds__(NT, 2) void conv_x3_gnb_kernel(ConvParams p, GnbParams g) {
+  conv_x3_body<XF_NONE, false, TW, NPROD, true>(p, g);
+}
+
+template <int XF, bool SKIP, int TW, int NPROD>
 static int launch_x3_inst(const ConvParams& p, hipStream_t stream) {
   static bool attr_set[kMaxDevices] = {};
   const size_t lds = (size_t)X_LDS_FLOATS * sizeof(float);
@@ -1160,6 +1278,19 @@ static int launch_x3_inst(const ConvParams& p, hipStream_t stream) {
   const int nunit = p.npix_tiles * (p.cout_pad / XBN) * p.ksplit;
   const int grid = nunit < ncu ? nunit : ncu;  // one workgroup per CU (LDS-bound)
   hipLaunchKernelGGL((conv_x3_kernel<XF, SKIP, TW, NPROD>), dim3(grid), dim3(NT), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
+template <int TW, int NPROD>
+static int launch_x3_gnb_inst(const ConvParams& p, const GnbParams& g, hipStream_t stream) {
+  static bool attr_set[kMaxDevices] = {};
+  const size_t lds = (size_t)X_LDS_FLOATS * sizeof(float);
+  hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_x3_gnb_kernel<TW, NPROD>), (int)lds);
+  if (e != hipSuccess) return (int)e;
+  const int ncu = device_cu_count();
+  const int nunit = p.npix_tiles * (p.cout_pad / XBN) * p.ksplit;
+  const int grid = nunit < ncu ? nunit : ncu;
+  hipLaunchKernelGGL((conv_x3_gnb_kernel<TW, NPROD>), dim3(grid), dim3(NT), lds, stream, p, g);
   return (int)hipGetLastError();
 }
 
@@ -1193,6 +1324,15 @@ bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
          (!p.wskip || (p.sc0 % XSK == 0 && p.sc1 % XSK == 0 && p.cs_pad == p.sc0 + p.sc1)) &&
          p.ksplit >= 1 && nch % p.ksplit == 0 && (!p.res || p.res_xform != XF_DOWN || p.ksplit > 1) &&
          (!p.wskip || !p.res || p.ksplit > 1);  // a SKIP kernel's residual goes through the split-K reduction
+}
+
+// Eligible as conv_x3_eligible plus: single-image 256-pixel tiles (TW 32 or 16), no split-K, no residual, no
+// 1x1 segment, XF_NONE (the host checks with conv_x3_eligible first).
+int launch_conv_x3_gnb(const ConvParams& p, const GnbParams& g, hipStream_t stream) {
+  if (p.ksplit != 1 || p.IMGS != 1 || p.res || p.wskip || !g.part || !g.x0 || !g.stats || (p.TW != 32 && p.TW != 16))
+    return (int)hipErrorInvalidValue;
+  if (p.x3_nprod == 1) return p.TW == 32 ? launch_x3_gnb_inst<32, 1>(p, g, stream) : launch_x3_gnb_inst<16, 1>(p, g, stream);
+  return p.TW == 32 ? launch_x3_gnb_inst<32, 3>(p, g, stream) : launch_x3_gnb_inst<16, 3>(p, g, stream);
 }
 
 int launch_conv_x3(const ConvParams& p, int xform, hipStream_t stream) {

@@ -2164,8 +2164,9 @@ static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, 
                        const float* bias, int cin_pad, int cout, const float* res, float* out, float* part,
                        int64_t part_floats, unsigned* guard, int wx3_taps, float* gstat, int64_t gstat_floats,
                        int* gstat_E, float* gstat_cnt, int nprod, void* stream, const float* actA = nullptr,
-                       const float* actB = nullptr) {
+                       const float* actB = nullptr, GnbParams* gnb = nullptr, int* gnb_nsl = nullptr) {
   if (gstat_E) *gstat_E = 0;
+  if (gnb_nsl) *gnb_nsl = 0;
   if ((H & (H - 1)) || c0 + c1 != cin_pad || !x0 || !out || !wx3 || !bias || !guard || (nprod != 1 && nprod != 3)) {
     set_error("ifd_tr_conv_x3: unsupported arguments");
     return 2;
@@ -2211,7 +2212,15 @@ static int conv_x3_run(const float* x0, int c0, const float* x1, int c1, int N, 
     p.gstat = gstat;
     p.gstat_E = p.tiles_x * p.tiles_y * 4;
   }
-  int e = launch_conv_x3(p, XF_NONE, (hipStream_t)stream);
+  int e;
+  if (gnb && gnb_nsl && p.ksplit == 1 && p.IMGS == 1 && (p.TW == 32 || p.TW == 16) && !res && taps == 9 && !p.gstat) {
+    // the dgrad + its GroupNorm backward's pass-1 partial sums in the epilogue (conv.h GnbParams)
+    gnb->nsl = p.tiles_x * p.tiles_y * 4;
+    e = launch_conv_x3_gnb(p, *gnb, (hipStream_t)stream);
+    if (!e) *gnb_nsl = gnb->nsl;
+  } else {
+    e = launch_conv_x3(p, XF_NONE, (hipStream_t)stream);
+  }
   if (!e && p.gstat) {
     *gstat_E = p.gstat_E;
     *gstat_cnt = 256.f;
@@ -2247,6 +2256,30 @@ int ifd_tr_conv_x3_gn(const float* x0, int c0, const float* x1, int c1, int N, i
                       int64_t gstat_floats, int* gstat_E, float* gstat_cnt, int nprod, void* stream) {
   return conv_x3_run(x0, c0, x1, c1, N, H, wx3, bias, cin_pad, cout, res, out, part, part_floats, guard, 9, gstat,
                      gstat_floats, gstat_E, gstat_cnt, nprod, stream, actA, actB);
+}
+
+int64_t ifd_tr_gnb_part_floats(int N, int H, int cout) {
+  const int64_t HW = (int64_t)H * H;
+  return (int64_t)N * (HW >= 64 ? HW / 64 : 1) * cout * 3;
+}
+
+int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, const float* bias, int cin_pad,
+                       int cout, float* out, float* part, int64_t part_floats, unsigned* guard, const float* gx0, int gc0,
+                       const float* gx1, const float* stats, const float* gamma, const float* beta, const float* ss,
+                       int ss_stride, int act_silu, float* gpart, int64_t gpart_floats, int* gpart_nsl, int nprod,
+                       void* stream) {
+  if (!gpart_nsl || !gx0 || !stats || !gamma || !beta || gc0 <= 0 || gc0 > cout || (gc0 < cout && !gx1) ||
+      cout % 32 || ifd_tr_gnb_part_floats(N, H, cout) > gpart_floats || !gpart) {
+    set_error("ifd_tr_conv_x3_gnb: bad GroupNorm arguments or partial-sum buffer too small");
+    return 2;
+  }
+  GnbParams g{};
+  g.x0 = gx0; g.x1 = gx1; g.c0 = gc0;
+  g.stats = stats; g.gamma = gamma; g.beta = beta;
+  g.ss = ss; g.ss_stride = ss_stride; g.silu = act_silu;
+  g.part = gpart;
+  return conv_x3_run(dy, cdy, nullptr, 0, N, H, wx3, bias, cin_pad, cout, nullptr, out, part, part_floats, guard, 9,
+                     nullptr, 0, nullptr, nullptr, nprod, stream, nullptr, nullptr, &g, gpart_nsl);
 }
 
 int64_t ifd_tr_gstat_floats(int N, int H, int cout) {
@@ -2519,6 +2552,28 @@ int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gn_bwd_partial_kernel, dim3(nsl, N), dim3(256), 0, s, a, part);
   hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(grid1(N * C)), dim3(TB), 0, s, a, part, nsl, nc, dss);
+  hipLaunchKernelGGL(gn_bwd_group_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, a, nc, red);
+  hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
+  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl, N), dim3(256), 0, s, a, red, dx, accumulate);
+  return TR_LAST();
+}
+
+int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
+                            const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
+                            const float* stats, const float* part, int part_nsl, float* dx, int accumulate,
+                            float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream) {
+  const int64_t need = (int64_t)N * C * 3 + (int64_t)N * 64;
+  const int nsl = gn_nsl(HW, N, C);  // the dx pass keeps its own pixel slices
+  if (C % 32 || C > 1024 || need > work_floats || C0 % 4 || C0 <= 0 || C0 > C || (C0 < C && !x1) || !part ||
+      part_nsl <= 0) {
+    set_error("ifd_tr_gn_bwd_from_part: bad arguments or work too small");
+    return 2;
+  }
+  GnBwdArgs a{dout, x0, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, x1, C0};
+  float* nc = work;
+  float* red = nc + (int64_t)N * C * 3;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(grid1(N * C)), dim3(TB), 0, s, a, part, part_nsl, nc, dss);
   hipLaunchKernelGGL(gn_bwd_group_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, a, nc, red);
   hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
   hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl, N), dim3(256), 0, s, a, red, dx, accumulate);

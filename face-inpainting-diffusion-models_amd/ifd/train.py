@@ -51,6 +51,11 @@ TRAIN_EXPORTS = {
     "ifd_tr_gn_bwd_cat": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, i64,
                                 vp]),
     "ifd_tr_gn_slices": (i64, [i32, i32, i32]),
+    "ifd_tr_gnb_part_floats": (i64, [i32, i32, i32]),
+    "ifd_tr_conv_x3_gnb": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp, vp, vp, vp, i32,
+                                 i32, vp, i64, _c.POINTER(i32), i32, vp]),
+    "ifd_tr_gn_bwd_from_part": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, i32, vp, vp,
+                                      vp, vp, i64, vp]),
     "ifd_tr_gn_coef": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, i32, f32, vp, vp, vp, vp, i64, vp]),
     "ifd_tr_act_apply": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp]),
     "ifd_tr_head_x3_pack_floats": (i64, [i32]),
@@ -133,13 +138,17 @@ class UNetTrainer:
     the output head) is not materialised: ifd_tr_gn_coef gives per-(image, channel) coefficients A, B,
     the forward conv applies silu(A x + B) to the raw input on load (the sampler's prologue) and the
     weight gradient recomputes it at staging (ifd_tr_conv_wgrad_x3_gn). Shapes a kernel does not take
-    materialise the activation (ifd_tr_act_apply) and run the plain path."""
+    materialise the activation (ifd_tr_act_apply) and run the plain path.
+
+    fuse_gnb (split modes): the dgrad conv whose output feeds a GroupNorm backward (ResBlock out_layers.3 ->
+    out_layers.0, in_layers.2 -> in_layers.0 without resampling) computes that backward's pass-1 partial sums in
+    its epilogue (ifd_tr_conv_x3_gnb): the pass over (dout, x) of ifd_tr_gn_bwd is not run."""
 
     SPLIT_MODES = ("3xf16", "f16")
 
     def __init__(self, cfg: UNetConfig = FULL, device="cuda", lr=5e-5, weight_decay=0.01, betas=(0.9, 0.999),
                  eps=1e-8, max_norm=1.0, precision="fp32", x3_dgrad=True, x3_wgrad=True, x3_loss_scale_log2=20,
-                 fuse_gn=True):
+                 fuse_gn=True, fuse_gnb=True):
         if precision not in ("fp32", "3xf16", "f16"):
             raise ValueError(f"precision must be 'fp32', '3xf16' or 'f16', got {precision!r}")
         self.precision = precision
@@ -147,6 +156,7 @@ class UNetTrainer:
         self.x3_wgrad = bool(x3_wgrad)
         self.x3_loss_scale_log2 = int(x3_loss_scale_log2)
         self.fuse_gn = bool(fuse_gn)
+        self.fuse_gnb = bool(fuse_gnb)
         self.guard_trips = 0
         self.cfg = cfg
         self.dev = torch.device(device)
@@ -476,6 +486,62 @@ class UNetTrainer:
                                     P(self.g(prefix + "bias")), P(dss), P(work), work.numel(), self.s))
         return dx
 
+    def dgrad_gn_bwd(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None,
+                     silu=True, x1=None, C0=None):
+        """gn_bwd(conv^T(dy)) - the dgrad of conv `wname` fed into the GroupNorm backward of its input x (C
+        channels; x1 / C0 as gn_bwd). On the split kernel the GroupNorm's pass 1 runs in the dgrad's epilogue
+        (ifd_tr_conv_x3_gnb); shapes it does not take run conv() then gn_bwd()."""
+        out = self._dgrad_gnb(dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0)
+        if out is not None:
+            return out
+        da = self.conv(dy, cdy, N, H, wname, transpose=True)
+        return self.gn_bwd(da, x, N, H * H, C, prefix, stats, dx=dx, ss=ss, ss_stride=ss_stride, dss=dss, silu=silu,
+                           x1=x1, C0=C0)
+
+    def _dgrad_gnb(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0):
+        if not (self.fuse_gnb and self._x3_active(True)):
+            return None
+        w = self.p(wname)
+        if w.dim() != 4 or tuple(w.shape[2:]) != (3, 3):
+            return None
+        cout, cin = w.shape[0], w.shape[1]  # the dgrad maps cout -> cin channels
+        if cin != C or cin % 64 or ((cin // 64) & (cin // 64 - 1)) or cdy != _pad(cout, 16) or cdy % 16:
+            return None
+        key = (wname, 1, "x3")
+        wx3 = self._pack_cache.get(key)
+        if wx3 is None:
+            wx3 = self._empty(cin * cdy * 9)
+            chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, 9, cdy, cin, 1, P(wx3), P(self._guard), self.s))
+            self._pack_cache[key] = wx3
+        da = self._empty(N, H, H, cin)
+        pf = lib().ifd_tr_conv_x3_part_floats(N, H, cdy, cin)
+        part = self._empty(max(pf, 1))
+        gpf = lib().ifd_tr_gnb_part_floats(N, H, cin)
+        gpart = self._empty(gpf)
+        nsl = _c.c_int(0)
+        c0 = C0 if x1 is not None else C
+        gam, bet = self.p(prefix + "weight"), self.p(prefix + "bias")
+        rc = lib().ifd_tr_conv_x3_gnb(P(dy), cdy, N, H, P(wx3), P(self._zero_bias), cdy, cin, P(da), P(part), pf,
+                                      P(self._guard), P(x), c0, P(x1), P(stats), P(gam), P(bet), P(ss), ss_stride,
+                                      int(silu), P(gpart), gpf, _c.byref(nsl), self._nprod(), self.s)
+        if rc == 3:
+            return None
+        chk(rc)
+        if nsl.value == 0:  # (the conv ran; its geometry could not carry the partial sums)
+            return self.gn_bwd(da, x, N, H * H, C, prefix, stats, dx=dx, ss=ss, ss_stride=ss_stride, dss=dss,
+                               silu=silu, x1=x1, C0=C0)
+        acc = dx is not None
+        if dx is None:
+            dx = self._empty(N * H * H * C)
+        else:
+            self._dirty(dx)
+        work = self._empty(N * C * 3 + N * 64)
+        chk(lib().ifd_tr_gn_bwd_from_part(P(da), P(x), c0, P(x1), N, H * H, C, P(gam), P(bet), P(ss), ss_stride,
+                                          int(silu), P(stats), P(gpart), nsl.value, P(dx), int(acc),
+                                          P(self.g(prefix + "weight")), P(self.g(prefix + "bias")), P(dss), P(work),
+                                          work.numel(), self.s))
+        return dx
+
     def resample(self, x, N, Hin, C, mode):
         Ho = 2 * Hin if mode == 1 else Hin // 2
         out = self._empty(N, Ho, Ho, C)
@@ -660,7 +726,7 @@ class UNetTrainer:
             self.wgrad(dout6, co, so["x"], hc, N, H, "out.2.weight", "out.2.bias", gn=so["gn"])
         else:
             self.wgrad(dout6, co, so["a"], hc, N, H, "out.2.weight", "out.2.bias")
-        da = None
+        da = dh = None
         if self._x3_active(True) and co % 16:
             # the split kernel's dgrad reads 16-channel chunks: the head gradient padded with zero channels
             # (else the 8-channel dgrad runs on the fp32 kernel, ~4x the split kernel's time at 256^2).
@@ -668,10 +734,14 @@ class UNetTrainer:
             # model_channels not a multiple of 64) the fp32 kernel runs on the unpadded gradient.
             d16 = self._zeros(N, H, H, 16)
             self.copy_ch(dout6, co, 0, d16, 16, 0, co, N * H * H, False)
-            da = self._conv_x3(d16, 16, N, H, "out.2.weight", None, None, None, 0, True)
-        if da is None:
-            da = self.conv(dout6, co, N, H, "out.2.weight", transpose=True)
-        dh = self.gn_bwd(da, so["x"], N, H * H, hc, "out.0.", so["stats"], silu=True)
+            dh = self._dgrad_gnb(d16, 16, N, H, "out.2.weight", so["x"], hc, "out.0.", so["stats"], None, None, 0,
+                                 None, True, None, None)
+            if dh is None:
+                da = self._conv_x3(d16, 16, N, H, "out.2.weight", None, None, None, 0, True)
+        if dh is None:
+            if da is None:
+                da = self.conv(dout6, co, N, H, "out.2.weight", transpose=True)
+            dh = self.gn_bwd(da, so["x"], N, H * H, hc, "out.0.", so["stats"], silu=True)
         # hs gradients from the output blocks' skip inputs
         in_blocks = [b for b in self.plan if b[0] == "input"]
         dhs = [None] * len(in_blocks)
@@ -737,10 +807,9 @@ class UNetTrainer:
                        gn=sv["g2"])
         else:
             self.wgrad(dout, cout, sv["a2"], cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias")
-        da2 = self.conv(dout, cout, N, ro, p + "out_layers.3.weight", transpose=True)
         dE = self._zeros(N, 2 * cout)
-        dh1 = self.gn_bwd(da2, sv["h1"], N, ro * ro, cout, p + "out_layers.0.", sv["st2"], ss=sv["E"],
-                          ss_stride=2 * cout, dss=dE, silu=True)
+        dh1 = self.dgrad_gn_bwd(dout, cout, N, ro, p + "out_layers.3.weight", sv["h1"], cout, p + "out_layers.0.",
+                                sv["st2"], ss=sv["E"], ss_stride=2 * cout, dss=dE, silu=True)
         self.linear_bwd(dE, self._tape["emb"], N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True,
                         dx=demb)
         x1, c1 = sv.get("x1"), sv.get("c1", 0)
@@ -750,8 +819,9 @@ class UNetTrainer:
                        x1=x1, c1=c1)
         else:
             self.wgrad(dh1, cout, sv["a1r"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
-        da1r = self.conv(dh1, cout, N, ro, p + "in_layers.2.weight", transpose=True)
-        da1 = self.resample_bwd(da1r, N, r, cin, mode) if mode else da1r
+        if mode:
+            da1r = self.conv(dh1, cout, N, ro, p + "in_layers.2.weight", transpose=True)
+            da1 = self.resample_bwd(da1r, N, r, cin, mode)
         if cin != cout:
             self.wgrad(dout, cout, sv["xr"], c0, N, ro, p + "skip_connection.weight", p + "skip_connection.bias",
                        x1=x1, c1=c1)
@@ -763,9 +833,10 @@ class UNetTrainer:
             self.resample_bwd(dxr, N, r, cin, mode, dx=dx)
         else:
             # the skip path's gradient (dout itself, or the 1x1 conv's fresh dgrad) is the accumulation
-            # target of the GroupNorm input gradient: no separate add pass
-            dx = self.gn_bwd(da1, sv["x"], N, r * r, cin, p + "in_layers.0.", sv["st1"], dx=dxr, silu=True, x1=x1,
-                             C0=c0)
+            # target of the GroupNorm input gradient: no separate add pass; the dgrad of in_layers.2 carries
+            # the GroupNorm backward's pass 1 (dgrad_gn_bwd)
+            dx = self.dgrad_gn_bwd(dh1, cout, N, ro, p + "in_layers.2.weight", sv["x"], cin, p + "in_layers.0.",
+                                   sv["st1"], dx=dxr, silu=True, x1=x1, C0=c0)
         return dx, r
 
     # ------------------------------------------------------------------ loss / step
@@ -894,6 +965,7 @@ class BlockTrainer(UNetTrainer):
         self.precision, self.x3_dgrad, self.x3_loss_scale_log2, self.guard_trips = "fp32", False, 0, 0
         self.x3_wgrad = False
         self.fuse_gn = True  # (no effect in fp32: GroupNorm on load is a split-mode path)
+        self.fuse_gnb = True
         self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
         self._grad_clean = False
         self._pack_cache = {}

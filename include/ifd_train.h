@@ -143,6 +143,24 @@ int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x
                       const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                       const float* stats, float* dx, int accumulate, float* dgamma, float* dbeta, float* dss,
                       float* work, int64_t work_floats, void* stream);
+/* The dgrad conv that feeds a GroupNorm backward, with that backward's pass 1 fused into its epilogue
+ * (code/train_inpainting.py:15-79 backward of nn.py:46-48,151-152,203-207): out = conv^T(dy) on the split
+ * kernel (ifd_tr_conv_x3_taps, 3x3, no residual), and for GroupNorm input x = concat(gx0[gc0], gx1) (cout
+ * channels), stats / gamma / beta / ss as ifd_tr_gn_bwd: gpart[N][*gpart_nsl][cout][3] = per 64-pixel block
+ * sum dz, sum dz nrm, sum dz (1 + s) xhat. *gpart_nsl = 0 when the geometry cannot fuse (split-K, 8x8 tiles):
+ * the conv still ran, and the caller runs ifd_tr_gn_bwd_cat. gpart: ifd_tr_gnb_part_floats floats. */
+int64_t ifd_tr_gnb_part_floats(int N, int H, int cout);
+int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, const float* bias, int cin_pad,
+                       int cout, float* out, float* part, int64_t part_floats, unsigned* guard, const float* gx0, int gc0,
+                       const float* gx1, const float* stats, const float* gamma, const float* beta, const float* ss,
+                       int ss_stride, int act_silu, float* gpart, int64_t gpart_floats, int* gpart_nsl, int nprod,
+                       void* stream);
+/* ifd_tr_gn_bwd_cat with pass 1 done (gpart from ifd_tr_conv_x3_gnb): reduce, group, parameter and dx passes.
+ * work: N*C*3 + N*64 floats. */
+int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
+                            const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
+                            const float* stats, const float* part, int part_nsl, float* dx, int accumulate,
+                            float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream);
 /* nearest-up x2 (mode 1) / AvgPool2d(2) (mode 2) (code/nn.py:92-133) and the adjoint (dx at Hin). */
 int ifd_tr_resample(const float* x, int N, int Hin, int C, int mode, float* out, void* stream);
 int ifd_tr_resample_bwd(const float* dy, int N, int Hin, int C, int mode, float* dx, int accumulate, void* stream);

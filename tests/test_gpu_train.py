@@ -209,6 +209,15 @@ def test_train_x3_head_dgrad_fallback(record):
                     return None
                 return _orig(x, cin_x, N, H, name, bias_name, r, x1, c1, transpose, **kw)
             tr._conv_x3 = conv_x3
+            orig_gnb = tr._dgrad_gnb
+
+            def dgrad_gnb(dy, cdy, N, H, wname, *a, _orig=orig_gnb):
+                # the fused dgrad + GroupNorm-backward path is the split kernel too: declined as well
+                if wname == "out.2.weight":
+                    declined.append(("gnb", cdy))
+                    return None
+                return _orig(dy, cdy, N, H, wname, *a)
+            tr._dgrad_gnb = dgrad_gnb
         torch.manual_seed(11)
         t = torch.randint(0, 1000, (2,), device=DEV)
         noise = torch.randn(2, 3, cfg.image_size, cfg.image_size, device=DEV)
@@ -217,9 +226,10 @@ def test_train_x3_head_dgrad_fallback(record):
         torch.cuda.synchronize()
         assert tr.guard_trips == 0
         if decline:
-            # the padded operand was offered and declined; conv() then offers the unpadded 8-channel
-            # gradient (declined too) and runs the fp32 kernel on it
-            assert declined == [16, 8]
+            # the padded operand was offered (to the fused dgrad + GroupNorm backward, then to the plain split
+            # dgrad) and declined; conv() then offers the unpadded 8-channel gradient (declined too) and runs
+            # the fp32 kernel on it
+            assert declined == [("gnb", 16), 16, 8]
         res[prec] = (loss, tr.grad.clone(), tr.offsets)
         del tr
     (l32, g32, offs), (l3, g3, _) = res["fp32"], res["3xf16"]

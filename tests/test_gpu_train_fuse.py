@@ -155,6 +155,97 @@ def test_train_fuse_gn_step_matches_unfused(record):
     assert worst <= 1e-5, (worst, wname)
 
 
+def test_train_fuse_gnb_step_matches_unfused(record):
+    """Full config, B = 4: the 3xf16 step with the GroupNorm backward's pass 1 in the dgrad conv's epilogue
+    (fuse_gnb, ifd_tr_conv_x3_gnb + ifd_tr_gn_bwd_from_part) vs the separate partial pass. The partial sums run
+    over other pixel blocks (64-pixel wave blocks vs 256-pixel slices), so the gate is a tolerance: loss equal
+    (the forward is the same), every parameter gradient rel-L2 <= 1e-5."""
+    from test_gpu_train import _full_step
+    res = {}
+    for fuse in (False, True):
+        tr, loss = _full_step("3xf16", fuse_gnb=fuse)
+        assert tr.guard_trips == 0
+        res[fuse] = (loss, tr.grad.clone(), tr.offsets)
+        del tr
+    (l0, g0, offs), (l1, g1, _) = res[False], res[True]
+    worst, wname = 0.0, None
+    for k, (o, shape) in offs.items():
+        n = int(np.prod(shape))
+        b = g0[o:o + n].double()
+        if float(b.norm()) > 0:
+            r = float((g1[o:o + n].double() - b).norm() / b.norm())
+            if r > worst:
+                worst, wname = r, k
+    record("train_fuse/step_gnb_vs_separate", rel_loss=abs(l1 - l0) / abs(l0), max_tensor_grad_rel=worst,
+           worst_tensor=wname)
+    assert l1 == l0
+    assert worst <= 1e-5, (worst, wname)
+
+
+def test_conv_x3_gnb_partials_match_separate_pass(record):
+    """ifd_tr_conv_x3_gnb's partial sums, reduced, against ifd_tr_gn_bwd_cat's (same dgrad output, same x): the
+    whole GroupNorm backward from the fused partials equals the separate pass's to rel-L2 1e-6 (dx, dgamma,
+    dbeta, dscale/shift), for a single source with scale/shift and for a two-source concat input."""
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    # (shapes with >= 256 units, so the geometry takes no split-K: the fused path)
+    for (N, H, cdy, C, C0, use_ss) in ((8, 64, 128, 128, 128, True), (16, 32, 128, 256, 128, False)):
+        g = torch.Generator().manual_seed(N * H + C)
+        dy = torch.randn(N, H, H, cdy, generator=g).to(DEV)
+        w = (torch.randn(cdy, C, 3, 3, generator=g) / (3 * C ** 0.5)).to(DEV)  # forward conv C -> cdy; dgrad cdy -> C
+        x = (torch.randn(N, H, H, C, generator=g) + 0.2).to(DEV)
+        x0, x1 = x[..., :C0].contiguous(), (x[..., C0:].contiguous() if C0 < C else None)
+        gam = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+        bet = (0.1 * torch.randn(C, generator=g)).to(DEV)
+        ss = (0.1 * torch.randn(N, 2 * C, generator=g)).to(DEV) if use_ss else None
+        st = torch.empty(N * 64, device=DEV)
+        nsl0 = lib().ifd_tr_gn_slices(H * H, N, C)
+        work = torch.empty(N * nsl0 * 64, device=DEV, dtype=torch.float64)
+        out = torch.empty(N, H * H, C, device=DEV)
+        chk(lib().ifd_tr_gn_fwd(P(x), N, H * H, C, P(gam), P(bet), P(ss), 2 * C if use_ss else 0, 1, P(out), P(st),
+                                P(work), work.numel(), s))
+        wx3 = torch.empty(C * cdy * 9, device=DEV)
+        guard = torch.zeros(4, device=DEV, dtype=torch.int32)
+        chk(lib().ifd_tr_pack_conv_x3(P(w), cdy, C, 9, cdy, C, 1, P(wx3), P(guard), s))
+        zb = torch.zeros(4096, device=DEV)
+        pf = lib().ifd_tr_conv_x3_part_floats(N, H, cdy, C)
+        part = torch.empty(max(pf, 1), device=DEV)
+        da = torch.empty(N, H, H, C, device=DEV)
+        gpf = lib().ifd_tr_gnb_part_floats(N, H, C)
+        gpart = torch.empty(gpf, device=DEV)
+        nsl = ctypes.c_int(0)
+        chk(lib().ifd_tr_conv_x3_gnb(P(dy), cdy, N, H, P(wx3), P(zb), cdy, C, P(da), P(part), pf, P(guard), P(x0), C0,
+                                     P(x1), P(st), P(gam), P(bet), P(ss), 2 * C if use_ss else 0, 1, P(gpart), gpf,
+                                     ctypes.byref(nsl), 3, s))
+        assert nsl.value == (H * H // 256) * 4, nsl.value
+        outs = {}
+        for fused in (False, True):
+            dx = torch.empty(N, H, H, C, device=DEV)
+            dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+            dss = torch.zeros(N, 2 * C, device=DEV) if use_ss else None
+            if fused:
+                wk = torch.empty(N * C * 3 + N * 64, device=DEV)
+                chk(lib().ifd_tr_gn_bwd_from_part(P(da), P(x0), C0, P(x1), N, H * H, C, P(gam), P(bet), P(ss),
+                                                  2 * C if use_ss else 0, 1, P(st), P(gpart), nsl.value, P(dx), 0, P(dg),
+                                                  P(db), P(dss), P(wk), wk.numel(), s))
+            else:
+                wk = torch.empty(N * nsl0 * C * 3 + N * C * 3 + N * 64, device=DEV)
+                chk(lib().ifd_tr_gn_bwd_cat(P(da), P(x0), C0, P(x1), N, H * H, C, P(gam), P(bet), P(ss),
+                                            2 * C if use_ss else 0, 1, P(st), P(dx), 0, P(dg), P(db), P(dss), P(wk),
+                                            wk.numel(), s))
+            torch.cuda.synchronize()
+            outs[fused] = (dx, dg, db, dss)
+        assert int(guard.max()) == 0
+        for name, a, b in zip(("dx", "dgamma", "dbeta", "dss"), outs[True], outs[False]):
+            if b is None:
+                continue
+            r = float((a.double() - b.double()).norm() / b.double().norm())
+            record(f"train_fuse/gnb/{N}x{H}x{cdy}->{C}(C0={C0})/{name}", rel_l2=r)
+            assert r <= 1e-6, (name, r)
+
+
 @pytest.mark.parametrize("N,H,cin", [(2, 32, 128), (3, 16, 64)])
 def test_head_x3_matches_fp32(N, H, cin, record):
     """ifd_tr_conv_head_x3 (the split head kernel, NHWC 8 channels) vs the fp32 conv kernel with the same
