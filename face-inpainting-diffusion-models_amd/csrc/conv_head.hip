@@ -181,135 +181,234 @@ __global__ __launch_bounds__(HD_NT, 2) void conv_head_kernel(ConvParams p, const
 
 
 // ---- 3xf16 output head (the 3xf16 precision mode): the same conv on f16 MFMAs with split operands ----
-// The VALU head above reaches ~40 TFLOP/s (0.36 ms per eval at B = 16). Here persistent blocks (two
-// per CU) keep ALL the head's split weights in LDS ([chunk][tap][part][8 co][32 ch] f16: 36 KiB for
-// 128 channels, co 6, 7 zero) and walk 16 x 16-pixel tiles: per 32-channel chunk the 256 threads stage
-// the activated, split 18 x 18 halo ([part][px][32 ch] f16), then wave w computes tile rows 4w..4w+3
-// as 16-pixel M blocks with v_mfma_f32_16x16x32_f16 (N = 16 output channels, 6 used), three split
-// products per MAC as conv_x3.hip (weights x 2^11). The next chunk's halo loads are in registers
-// while the MFMAs run. The epilogue transposes the accumulators through LDS so each thread finishes
-// one pixel with the VALU head's epilogue (bias, NCHW store or the fused DDIM / DDPM step).
+// The VALU head above reaches ~40 TFLOP/s (0.36 ms per eval at B = 16). Here a persistent block per CU keeps
+// ALL the head's split weights in LDS ([chunk][tap][part][8 co][32 ch] f16: 36 KiB for 128 channels, co 6, 7
+// zero) and walks 16 x 16-pixel tiles in 32-channel chunks, warp-specialised:
+// * waves 4-11 (producers, two per SIMD) stage chunk s — the activated, split 18 x 18 halo ([part][px][32 ch]
+//   f16, conv_x3.hip's split: the same roundings) — into halo buffer s & 1, with two register sets of loads
+//   (chunk s + 2's issued right after chunk s is staged);
+// * waves 0-3 (consumers) run chunk s - 1 from the other buffer: wave w computes tile rows 4w..4w+3 as
+//   16-pixel M blocks with v_mfma_f32_16x16x32_f16 (N = 16 output channels, 6 used), three split products
+//   per MAC as conv_x3.hip (weights x 2^11), hi x hi and the corrections in separate accumulators;
+// * one block barrier per chunk step. A finished tile's accumulators go through a transpose buffer (two, by
+//   tile parity) to the producers, which run the per-pixel epilogue (bias, NCHW / NHWC store or the fused
+//   DDIM / DDPM step) in the next step, its inputs loaded before that step's staging.
+// Every producer load is unconditional (padding pixels load a clamped neighbour, the steps past the last
+// chunk re-load it): with loads under branches hipcc's waitcnt merge fell back to vmcnt(0) and drained the
+// prefetch. (gfx950 counts global stores in vmcnt too.)
+// What bounds it (timing ablations): the producers' staging VALU — ~40 issue cycles per
+// staged value (affine, exp2, rcp, split) sharing each SIMD's issue with the consumers' MFMAs, which hold it
+// 8 of every 16 cycles. Without the staging the head takes 0.13 instead of 0.23 ms per eval; without its
+// loads 0.19; without the MFMAs 0.20. The round-2 layout (two 256-thread blocks per CU, staging and MFMAs
+// serialised by barriers) ran 0.234 ms; four producer waves 0.25.
 constexpr int HX_T = 16;                                  // tile 16 x 16
 constexpr int HX_HW = HX_T + 2, HX_NP = HX_HW * HX_HW;  // 324 halo pixels
 constexpr int HX_CH = 32;                                 // channels per chunk (one MFMA k-step)
-constexpr int HX_ITEMS = (HX_NP * 8 + 255) / 256;         // (pixel, quad) items per thread: 11
 constexpr int HX_MAXCH = 4;                               // chunks held in LDS (cin <= 128)
 constexpr int HX_WCO = 8;                                 // packed output channels (6 used; B lanes 8..15 read zeros)
 constexpr int HX_WCH = 9 * 2 * HX_WCO * HX_CH;            // f16 per chunk of packed weights
-constexpr int HX_A = 2 * HX_NP * HX_CH;                   // f16 per halo stage
 constexpr int HX_Z = 32;                                  // a zero row for the unused B lanes
-// weights + zero row + halo stage (the epilogue's transpose buffer reuses the halo stage): 78.4 KiB,
-// two blocks per CU
-constexpr size_t HX_LDS = (size_t)(HX_MAXCH * HX_WCH + HX_Z + HX_A) * 2;
-static_assert(256 * 8 * 4 <= HX_A * 2, "transpose buffer fits the halo stage");
 typedef _Float16 hx_h8 __attribute__((ext_vector_type(8)));
-typedef _Float16 hx_h4 __attribute__((ext_vector_type(4)));
 typedef float hx_f4 __attribute__((ext_vector_type(4)));
 typedef unsigned hx_u2 __attribute__((ext_vector_type(2)));
 
-template <int CO>
-__global__ __launch_bounds__(256, 2) void conv_head_x3_kernel(ConvParams p, const _Float16* __restrict__ wx) {
+#define HX_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+constexpr int HW_PT = 8 * 64;                          // producer threads (two waves per SIMD)
+constexpr int HW_NT = 256 + HW_PT;                    // 4 consumer + 8 producer waves
+constexpr int HW_ITEMS = (HX_NP * 8 + HW_PT - 1) / HW_PT;  // (pixel, quad) staging items per producer thread
+constexpr int HW_NPP = HW_ITEMS * HW_PT / 8;  // halo rows per plane incl. the last items' spill rows
+constexpr int HW_A = 2 * HW_NPP * HX_CH;  // f16 per halo stage
+constexpr int HW_OB = 256 * HX_WCO;       // floats per transpose buffer
+static_assert(HW_NPP >= HX_NP && HW_NPP % 8 == 0, "staging items fit the padded plane");
+// weights + zero row + two halo stages + two transpose buffers (150 KiB with 8 producer waves), one block per CU
+constexpr size_t HW_LDS = (size_t)(HX_MAXCH * HX_WCH + HX_Z + 2 * HW_A) * 2 + 2 * HW_OB * 4;
+
+// conv_x3.hip's split2: hi = f16(v) for the pair (one v_cvt_pk_f16_f32), lo = f16(v - hi) by v_fma_mix (v - hi
+// exact in fp32, rounded once): the values of two casts in 1.5 instead of ~4 VALU ops per value
+typedef _Float16 hx_h2 __attribute__((ext_vector_type(2)));
+typedef float hx_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void hx_split2(float v0, float v1, unsigned& h, unsigned& l) {
+  asm volatile("" : "+v"(v0), "+v"(v1));
+  h = __builtin_bit_cast(unsigned, __builtin_convertvector(hx_f2{v0, v1}, hx_h2));
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(l)
+      : "v"(v0), "v"(v1), "v"(h));
+}
+
+template <int CO, int ACT, int EPI>
+__global__ __launch_bounds__(HW_NT, 1) void conv_head_x3ws_kernel(ConvParams p, const _Float16* __restrict__ wx) {
   extern __shared__ __attribute__((aligned(16))) char hx_smem[];
   _Float16* Wl = reinterpret_cast<_Float16*>(hx_smem);
   _Float16* Zl = Wl + HX_MAXCH * HX_WCH;
-  _Float16* Al = Zl + HX_Z;
-  float* Ob = reinterpret_cast<float*>(Al);  // [256 px][8], after the tile's last MFMAs
+  _Float16* Al0 = Zl + HX_Z;                               // halo stage 0; stage 1 follows
+  float* Ob0 = reinterpret_cast<float*>(Al0 + 2 * HW_A);  // transpose buffer 0; buffer 1 follows
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cin = p.c0, nch = cin / HX_CH;
   const int tiles_x = p.W / HX_T, tiles_y = p.H / HX_T;
   const int ntiles = p.N * tiles_x * tiles_y;
-  // weights once per block
   {
     const hx_f4* src = reinterpret_cast<const hx_f4*>(wx);
     hx_f4* dst = reinterpret_cast<hx_f4*>(Wl);
-    for (int i = tid; i < nch * HX_WCH / 8; i += 256) dst[i] = src[i];
+    for (int i = tid; i < nch * HX_WCH / 8; i += HW_NT) dst[i] = src[i];
     if (tid < HX_Z / 8) reinterpret_cast<hx_f4*>(Zl)[tid] = hx_f4{0.f, 0.f, 0.f, 0.f};
   }
-  const int q = tid & 7;  // channel quad of every staging item
-  int hyv[HX_ITEMS], hxv[HX_ITEMS];
-#pragma unroll
-  for (int k = 0; k < HX_ITEMS; ++k) {
-    const int px = (tid + 256 * k) >> 3;
-    hyv[k] = px < HX_NP ? px / HX_HW : -1000000;
-    hxv[k] = px % HX_HW;
-  }
-  hx_f4 raw[HX_ITEMS], ca, cb;
-  float gmax = 0.f;
   auto tile_of = [&](int t, int& n, int& y0, int& x0) {
     x0 = (t % tiles_x) * HX_T;
     t /= tiles_x;
     y0 = (t % tiles_y) * HX_T;
     n = t / tiles_y;
   };
-  auto load = [&](int t, int c) {
-    int n, y0, x0;
-    tile_of(t, n, y0, x0);
-    const float* src = p.in0 + (size_t)n * p.H * p.W * cin + HX_CH * c + 4 * q;
+  const int nwork = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;  // >= 1 (grid <= ntiles)
+  const int nsteps = nwork * nch;  // chunk steps of this block
+  // step s: producers stage chunk s; consumers compute chunk s - 1; producers finish the tile whose last chunk
+  // was computed in step s - 1. Every wave runs the same (even) number of steps, one barrier each.
+  const int T = (nsteps + 3) & ~1;
+  if (wave >= 4) {
+    const int ptid = tid - 256;
+    const int q = ptid & 7;
+    int hyv[HW_ITEMS], hxv[HW_ITEMS], ldo[HW_ITEMS];
 #pragma unroll
-    for (int k = 0; k < HX_ITEMS; ++k) {
-      const int y = y0 + hyv[k] - 1, x = x0 + hxv[k] - 1;
-      const bool ok = y >= 0 && y < p.H && x >= 0 && x < p.W;
-      raw[k] = ok ? *reinterpret_cast<const hx_f4*>(src + ((size_t)y * p.W + x) * cin) : hx_f4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < HW_ITEMS; ++k) {
+      const int px = (ptid + HW_PT * k) >> 3;  // rows past the halo (the last item) are staged into spill rows
+      hyv[k] = px < HX_NP ? px / HX_HW : 0;
+      hxv[k] = px < HX_NP ? px % HX_HW : 0;
+      ldo[k] = px * HX_CH + 4 * q;
     }
-    ca = hx_f4{1.f, 1.f, 1.f, 1.f};
-    cb = hx_f4{0.f, 0.f, 0.f, 0.f};
-    if (p.act != ACT_NONE) {
-      ca = *reinterpret_cast<const hx_f4*>(p.actA + (size_t)n * cin + HX_CH * c + 4 * q);
-      cb = *reinterpret_cast<const hx_f4*>(p.actB + (size_t)n * cin + HX_CH * c + 4 * q);
-    }
-  };
-  auto stage = [&](int t) {
-    int n, y0, x0;
-    tile_of(t, n, y0, x0);
+    hx_f4 raw0[HW_ITEMS], raw1[HW_ITEMS], ca0, cb0, ca1, cb1;
+    float gmax = 0.f;
+    float bias[HX_WCO];  // in registers: read in the epilogue it would be re-read after every store (may alias)
 #pragma unroll
-    for (int k = 0; k < HX_ITEMS; ++k) {
-      const int px = (tid + 256 * k) >> 3;
-      if (px < HX_NP) {
+    for (int co = 0; co < HX_WCO; ++co) bias[co] = co < (EPI == EPI_NHWC ? HX_WCO : CO) ? p.bias[co] : 0.f;
+    auto load = [&](hx_f4 (&raw)[HW_ITEMS], hx_f4& ca, hx_f4& cb, int s) __attribute__((always_inline)) {
+      const int se = s < nsteps ? s : nsteps - 1;  // past the end: the last chunk again (unused)
+      int n, y0, x0;
+      const int c = se % nch;
+      tile_of(blockIdx.x + (se / nch) * gridDim.x, n, y0, x0);
+      if (ACT != ACT_NONE) {  // the coefficients first: older than the halo loads in the queue
+        ca = *reinterpret_cast<const hx_f4*>(p.actA + (size_t)n * cin + HX_CH * c + 4 * q);
+        cb = *reinterpret_cast<const hx_f4*>(p.actB + (size_t)n * cin + HX_CH * c + 4 * q);
+      }
+      const float* src = p.in0 + (size_t)n * p.H * p.W * cin + HX_CH * c + 4 * q;
+#pragma unroll
+      for (int k = 0; k < HW_ITEMS; ++k) {
+        const int y = min(max(y0 + hyv[k] - 1, 0), p.H - 1), x = min(max(x0 + hxv[k] - 1, 0), p.W - 1);
+        raw[k] = *reinterpret_cast<const hx_f4*>(src + ((size_t)y * p.W + x) * cin);
+      }
+    };
+    auto stage = [&](const hx_f4 (&raw)[HW_ITEMS], hx_f4 ca, hx_f4 cb, int s) __attribute__((always_inline)) {
+      int n, y0, x0;
+      tile_of(blockIdx.x + (s / nch) * gridDim.x, n, y0, x0);
+      _Float16* Al = Al0 + (s & 1) * HW_A;
+#pragma unroll
+      for (int k = 0; k < HW_ITEMS; ++k) {
         const int y = y0 + hyv[k] - 1, x = x0 + hxv[k] - 1;
         const bool ok = y >= 0 && y < p.H && x >= 0 && x < p.W;
-        hx_h4 hi, lo;
+        float v[4];
+        if (ACT == ACT_AFFINE_SILU) {
+          // the zero padding rides in the exponent (conv_x3.hip store_act): 2^(+inf) = inf, rcp(1 + inf) = 0
+          const float pinf = ok ? 0.f : __builtin_inff();
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float v = raw[k][j];
-          if (p.act != ACT_NONE) {
-            v = ca[j] * v + cb[j];
-            if (p.act == ACT_AFFINE_SILU) v = silu_fast(v);
+          for (int j = 0; j < 4; ++j) {
+            const float t = fmaf(ca[j], raw[k][j], cb[j]);
+            v[j] = t * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(fmaf(t, -1.4426950408889634f, pinf)));
           }
-          v = ok ? v : 0.f;  // zero padding of the activated input
-          asm volatile("" : "+v"(v));
-          gmax = fmaxf(gmax, fabsf(v));
-          const _Float16 hh = (_Float16)v;
-          hi[j] = hh;
-          lo[j] = (_Float16)(v - (float)hh);
-        }
-        *reinterpret_cast<hx_u2*>(Al + px * HX_CH + 4 * q) = __builtin_bit_cast(hx_u2, hi);
-        *reinterpret_cast<hx_u2*>(Al + HX_NP * HX_CH + px * HX_CH + 4 * q) = __builtin_bit_cast(hx_u2, lo);
-      }
-    }
-  };
-  // MFMA lane roles (16x16x32): A lane = pixel i (lane & 15) of a tile row, K group kg = lane >> 4
-  // (channels 8 kg .. 8 kg + 7); B lane = output channel j (lane & 15), same K group; C lane = channel
-  // j, pixels 4 kg .. 4 kg + 3 of the row
-  const int li = lane & 15, kg = lane >> 4;
-  const int nwork = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  if (nwork > 0) load(blockIdx.x, 0);
-  for (int u = 0; u < nwork; ++u) {
-    const int t = blockIdx.x + u * gridDim.x;
-    hx_f4 acc[4], accl[4];  // hi x hi products; the two correction products (added once per output)
+        } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = accl[r] = hx_f4{0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < nch; ++c) {
-      __syncthreads();  // previous chunk's MFMA reads (and the weight copy) done
-      stage(t);
-      __syncthreads();
-      // next chunk's (or next tile's first chunk's) loads in flight during the MFMAs
-      if (c + 1 < nch)
-        load(t, c + 1);
-      else if (u + 1 < nwork)
-        load(t + gridDim.x, 0);
+          for (int j = 0; j < 4; ++j) v[j] = ok ? (ACT == ACT_AFFINE ? fmaf(ca[j], raw[k][j], cb[j]) : raw[k][j]) : 0.f;
+        }
+        gmax = fmaxf(gmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        unsigned h0, l0, h1, l1;
+        hx_split2(v[0], v[1], h0, l0);
+        hx_split2(v[2], v[3], h1, l1);
+        *reinterpret_cast<hx_u2*>(Al + ldo[k]) = hx_u2{h0, h1};
+        *reinterpret_cast<hx_u2*>(Al + HW_NPP * HX_CH + ldo[k]) = hx_u2{l0, l1};
+      }
+    };
+    constexpr bool kStep = EPI == EPI_DDIM || EPI == EPI_DDPM;
+    const int HWp = p.H * p.W;
+    // the step epilogue's optional inputs read a valid stand-in when absent (no branch around the loads)
+    const float* gt_p = p.sc.inject ? p.gt : p.img;
+    const float* kn_p = p.sc.inject ? p.known : p.img;
+    const float* mk_p = p.sc.inject ? p.mask : p.img;
+    const float* nz_p = (EPI == EPI_DDPM || p.sc.use_noise) ? p.noise : p.img;
+    auto step = [&](hx_f4 (&raw)[HW_ITEMS], hx_f4& ca, hx_f4& cb, int s) __attribute__((always_inline)) {
+      // (the first 256 producer threads finish one pixel each)
+      const bool epi = s >= 2 && s - 2 < nsteps && (s - 2) % nch == nch - 1 && ptid < 256;
+      int je = (s - 2) / nch;
+      je = je < 0 ? 0 : (je >= nwork ? nwork - 1 : je);
+      int n, y0, x0;
+      tile_of(blockIdx.x + je * gridDim.x, n, y0, x0);
+      const int pt = ptid & 255;
+      const size_t pix = (size_t)(y0 + (pt >> 4)) * p.W + (x0 + (pt & 15));
+      float xi[3], gi[3], kn[3], nz[3], mk = 0.f;
+      if (kStep) {  // loaded every step (a stand-in tile when no epilogue is due)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const size_t o3 = ((size_t)n * 3 + c) * HWp + pix;
+          xi[c] = p.img[o3];
+          gi[c] = gt_p[o3];
+          kn[c] = kn_p[o3];
+          nz[c] = nz_p[o3];
+        }
+        mk = mk_p[p.sc.inject ? (size_t)n * HWp + pix : ((size_t)n * 3) * HWp + pix];
+      }
+      if (s < nsteps) stage(raw, ca, cb, s);
+      load(raw, ca, cb, s + 2);
+      if (epi) {
+        const float* Ob = Ob0 + (je & 1) * HW_OB;
+        float a[8];
+#pragma unroll
+        for (int co = 0; co < 8; ++co) a[co] = Ob[pt * 8 + co];
+        if (EPI == EPI_NCHW) {
+#pragma unroll
+          for (int co = 0; co < CO; ++co) p.out[((size_t)n * CO + co) * HWp + pix] = a[co] + bias[co];
+        } else if (EPI == EPI_NHWC) {  // the training forward: [N][H][W][8], the padded channels' rows zero
+          hx_f4* o = reinterpret_cast<hx_f4*>(p.out + ((size_t)n * HWp + pix) * HX_WCO);
+          o[0] = hx_f4{a[0] + bias[0], a[1] + bias[1], a[2] + bias[2], a[3] + bias[3]};
+          o[1] = hx_f4{a[4] + bias[4], a[5] + bias[5], a[6] + bias[6], a[7] + bias[7]};
+        } else {
+          if (!p.sc.inject) mk = 0.f;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const size_t o3 = ((size_t)n * 3 + c) * HWp + pix;
+            const float eps = a[c] + bias[c];
+            const float g = p.sc.inject ? gi[c] : 0.f, k = p.sc.inject ? kn[c] : 0.f;
+            float v;
+            if (EPI == EPI_DDIM) {
+              v = ddim_step_value(p.sc, xi[c], eps, p.sc.use_noise ? nz[c] : 0.f, g, mk, k);
+            } else {
+              const float var_v = a[CO > 3 ? c + 3 : c] + bias[c + 3];
+              v = ddpm_step_value(p.sc, xi[c], eps, var_v, nz[c], g, mk, k);
+            }
+            p.img[o3] = v;
+          }
+        }
+      }
+      HX_BARRIER();
+    };
+    load(raw0, ca0, cb0, 0);
+    load(raw1, ca1, cb1, 1);
+    // unrolled by two so each register set has one static name
+    for (int s = 0; s < T; s += 2) {
+      step(raw0, ca0, cb0, s);
+      step(raw1, ca1, cb1, s + 1);
+    }
+    if (p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
+    return;
+  }
+  // consumers. MFMA lane roles (16x16x32): A lane = pixel i (lane & 15) of a tile row, K group kg = lane >> 4
+  // (channels 8 kg .. 8 kg + 7); B lane = output channel j (lane & 15), same K group; C lane = channel j,
+  // pixels 4 kg .. 4 kg + 3 of the row
+  const int li = lane & 15, kg = lane >> 4;
+  hx_f4 acc[4], accl[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = accl[r] = hx_f4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < T; ++s) {
+    if (s >= 1 && s <= nsteps) {
+      const int cs = s - 1, c = cs % nch;
+      const _Float16* Al = Al0 + (cs & 1) * HW_A;
       const _Float16* Wc = Wl + c * HX_WCH;
-      // per kernel column kx: the 6 halo rows the wave's 4 tile rows need (A), then the 3 taps (ky) of
-      // the column; one column's fragments at a time keeps the live set within two waves per SIMD
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         hx_h8 ah[6], al[6];
@@ -317,7 +416,7 @@ __global__ __launch_bounds__(256, 2) void conv_head_x3_kernel(ConvParams p, cons
         for (int rr = 0; rr < 6; ++rr) {
           const int hp = (4 * wave + rr) * HX_HW + li + kx;
           ah[rr] = *reinterpret_cast<const hx_h8*>(Al + hp * HX_CH + 8 * kg);
-          al[rr] = *reinterpret_cast<const hx_h8*>(Al + HX_NP * HX_CH + hp * HX_CH + 8 * kg);
+          al[rr] = *reinterpret_cast<const hx_h8*>(Al + HW_NPP * HX_CH + hp * HX_CH + 8 * kg);
         }
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
@@ -326,64 +425,33 @@ __global__ __launch_bounds__(256, 2) void conv_head_x3_kernel(ConvParams p, cons
           const _Float16* bp1 = li < HX_WCO ? Wc + ((tap * 2 + 1) * HX_WCO + li) * HX_CH + 8 * kg : Zl;
           const hx_h8 bh = *reinterpret_cast<const hx_h8*>(bp0);
           const hx_h8 bl = *reinterpret_cast<const hx_h8*>(bp1);
+          // one consumer wave per SIMD: the products grouped by kind, so each accumulator's next MFMA is four
+          // MFMAs behind its last
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bh, acc[r], 0, 0, 0);
-            accl[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bl, accl[r], 0, 0, 0);
-            accl[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[r + ky], bh, accl[r], 0, 0, 0);
-          }
+          for (int r = 0; r < 4; ++r) acc[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bh, acc[r], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) accl[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[r + ky], bl, accl[r], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) accl[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[r + ky], bh, accl[r], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-    }
-    // transpose: Ob[pixel][channel], pixel = tile row (4 wave + r) x 16 + column (4 kg + e); Ob is the
-    // halo stage, so every wave's MFMA reads must be done first
-    __syncthreads();
-    if (li < 8)
+      if (c == nch - 1) {
+        // Ob[pixel][channel], pixel = tile row (4 wave + r) x 16 + column (4 kg + e): the producers read it in
+        // the next step
+        float* Ob = Ob0 + ((cs / nch) & 1) * HW_OB;
+        if (li < 8)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+          for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Ob[((4 * wave + r) * HX_T + 4 * kg + e) * 8 + li] = (acc[r][e] + accl[r][e]) * (1.0f / 2048.0f);
-    __syncthreads();
-    {
-      int n, y0, x0;
-      tile_of(t, n, y0, x0);
-      const int HWp = p.H * p.W;
-      const size_t pix = (size_t)(y0 + (tid >> 4)) * p.W + (x0 + (tid & 15));
-      float a[8];
+            for (int e = 0; e < 4; ++e)
+              Ob[((4 * wave + r) * HX_T + 4 * kg + e) * 8 + li] = (acc[r][e] + accl[r][e]) * (1.0f / 2048.0f);
 #pragma unroll
-      for (int co = 0; co < 8; ++co) a[co] = Ob[tid * 8 + co];
-      if (p.epi == EPI_NCHW) {
-#pragma unroll
-        for (int co = 0; co < CO; ++co) p.out[((size_t)n * CO + co) * HWp + pix] = a[co] + p.bias[co];
-      } else if (p.epi == EPI_NHWC) {  // the training forward: [N][H][W][8], the padded channels' rows zero
-        hx_f4* o = reinterpret_cast<hx_f4*>(p.out + ((size_t)n * HWp + pix) * HX_WCO);
-        o[0] = hx_f4{a[0] + p.bias[0], a[1] + p.bias[1], a[2] + p.bias[2], a[3] + p.bias[3]};
-        o[1] = hx_f4{a[4] + p.bias[4], a[5] + p.bias[5], a[6] + p.bias[6], a[7] + p.bias[7]};
-      } else {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const size_t o3 = ((size_t)n * 3 + c) * HWp + pix;
-          const size_t om = (size_t)n * HWp + pix;
-          const float eps = a[c] + p.bias[c];
-          const float x = p.img[o3];
-          const float mk = p.sc.inject ? p.mask[om] : 0.f;
-          const float g = p.sc.inject ? p.gt[o3] : 0.f;
-          const float kn = p.sc.inject ? p.known[o3] : 0.f;
-          float v;
-          if (p.epi == EPI_DDIM) {
-            const float nz = p.sc.use_noise ? p.noise[o3] : 0.f;
-            v = ddim_step_value(p.sc, x, eps, nz, g, mk, kn);
-          } else {
-            const float var_v = a[CO > 3 ? c + 3 : c] + p.bias[c + 3];
-            v = ddpm_step_value(p.sc, x, eps, var_v, p.noise[o3], g, mk, kn);
-          }
-          p.img[o3] = v;
-        }
+        for (int r = 0; r < 4; ++r) acc[r] = accl[r] = hx_f4{0.f, 0.f, 0.f, 0.f};
       }
     }
+    HX_BARRIER();
   }
-  if (p.guard && gmax >= 65504.0f) atomicOr(p.guard, 1u);
 }
 }  // namespace
 
@@ -494,24 +562,43 @@ int launch_pack_head_x3(const float* w, int cout, int cin, float* dst, unsigned*
   return (int)hipGetLastError();
 }
 
+namespace {
+template <int CO, int ACT, int EPI>
+int launch_head_ws(const ConvParams& p, const float* wx, int grid, hipStream_t stream) {
+  static bool attr_set[kMaxDevices] = {};
+  const void* fn = reinterpret_cast<const void*>(&conv_head_x3ws_kernel<CO, ACT, EPI>);
+  hipError_t e = set_lds_attr_once(attr_set, fn, (int)HW_LDS);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL((conv_head_x3ws_kernel<CO, ACT, EPI>), dim3(grid), dim3(HW_NT), HW_LDS, stream, p,
+                     reinterpret_cast<const _Float16*>(wx));
+  return (int)hipGetLastError();
+}
+template <int CO, int ACT>
+int launch_head_ws_epi(const ConvParams& p, const float* wx, int grid, hipStream_t stream) {
+  switch (p.epi) {
+    case EPI_NCHW: return launch_head_ws<CO, ACT, EPI_NCHW>(p, wx, grid, stream);
+    case EPI_DDIM: return launch_head_ws<CO, ACT, EPI_DDIM>(p, wx, grid, stream);
+    case EPI_NHWC: if (CO == 6) return launch_head_ws<CO, ACT, EPI_NHWC>(p, wx, grid, stream); break;
+    case EPI_DDPM: if (CO == 6) return launch_head_ws<CO, ACT, EPI_DDPM>(p, wx, grid, stream); break;
+  }
+  return (int)hipErrorInvalidValue;
+}
+template <int CO>
+int launch_head_ws_act(const ConvParams& p, const float* wx, int grid, hipStream_t stream) {
+  if (p.act == ACT_AFFINE_SILU) return launch_head_ws_epi<CO, ACT_AFFINE_SILU>(p, wx, grid, stream);
+  if (p.act == ACT_AFFINE) return launch_head_ws_epi<CO, ACT_AFFINE>(p, wx, grid, stream);
+  return launch_head_ws_epi<CO, ACT_NONE>(p, wx, grid, stream);
+}
+}  // namespace
+
 int launch_conv_head_x3(const ConvParams& p, const float* wx, hipStream_t stream) {
   const int ntiles = p.N * (p.H / HX_T) * (p.W / HX_T);
-  const int ncu = 2 * device_cu_count();  // two blocks per CU
+  const int ncu = device_cu_count();  // one block per CU
   const int grid = ntiles < ncu ? ntiles : ncu;
-  if (p.cout == 6 || p.cout == HX_WCO) {  // (CO only shapes the NCHW / sampler epilogues)
-    static bool attr_set[kMaxDevices] = {};
-    hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_head_x3_kernel<6>), (int)HX_LDS);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(conv_head_x3_kernel<6>, dim3(grid), dim3(256), HX_LDS, stream, p,
-                       reinterpret_cast<const _Float16*>(wx));
-  } else {
-    static bool attr_set[kMaxDevices] = {};
-    hipError_t e = set_lds_attr_once(attr_set, reinterpret_cast<const void*>(&conv_head_x3_kernel<3>), (int)HX_LDS);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(conv_head_x3_kernel<3>, dim3(grid), dim3(256), HX_LDS, stream, p,
-                       reinterpret_cast<const _Float16*>(wx));
-  }
-  return (int)hipGetLastError();
+  if (grid <= 0) return 0;
+  // (CO only shapes the NCHW / sampler epilogues; the NHWC training head is CO 6 with 8 stored channels)
+  if (p.cout == 6 || p.cout == HX_WCO) return launch_head_ws_act<6>(p, wx, grid, stream);
+  return launch_head_ws_act<3>(p, wx, grid, stream);
 }
 
 }  // namespace ifd
