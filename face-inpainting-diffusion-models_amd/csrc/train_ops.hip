@@ -1004,6 +1004,22 @@ __global__ void slab_reduce_kernel(const float* __restrict__ part, int S, int64_
   for (int z = 1; z < S; ++z) s += part[(size_t)z * n + i];
   out[i] = accumulate ? out[i] + s : s;
 }
+// slab_reduce_kernel over the weight slabs and, in the threads past them, colsum_final_kernel's bias sums
+// (float64 over the split rows in order): one launch instead of two (84 per training step)
+__global__ void slab_bias_reduce_kernel(const float* __restrict__ part, int S, int64_t n, float* __restrict__ out,
+                                        const float* __restrict__ colpart, int C, float* __restrict__ db) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    float s = part[i];
+    for (int z = 1; z < S; ++z) s += part[(size_t)z * n + i];
+    out[i] += s;
+  } else if (i < n + C) {
+    const int c = (int)(i - n);
+    double s = 0.0;
+    for (int z = 0; z < S; ++z) s += colpart[(int64_t)z * C + c];
+    db[c] += (float)s;
+  }
+}
 
 // Column sums of an [P][C] tensor in a fixed order: stage 1 per (pixel slice, column) — a block is
 // 64 columns x 4 row lanes (each row lane strides the slice's pixels, coalesced along the columns),
@@ -1321,42 +1337,73 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnBwdArgs a, float*
     o[2] = t3;
   }
 }
-// per (n, c): A1..A3 (float64 over slices) -> dss, and per-(n, g) means -> red[n][g][2]
-__global__ void gn_bwd_reduce_kernel(GnBwdArgs a, const float* __restrict__ part, int nsl, float* __restrict__ nc,
-                                     float* __restrict__ dss) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (n, c)
-  if (i >= a.N * a.C) return;
-  const int n = i / a.C, c = i % a.C;
+// Per (n, c): A1..A3 (float64 over slices) -> nc, dss; per (n, g): the group means -> red[n][g][2]. One launch,
+// a block per (group, image) (round 5; was two launches): each of the group's channels is summed over the
+// slices by SL lanes in float64 (lane l takes slices l, l + SL, ...), the lanes combined by a fixed pairwise
+// tree, then the group's means from the float-rounded per-channel sums, in channel order. (A serial
+// per-channel loop over up to 256 slices took ~18 us a call.)
+__global__ __launch_bounds__(256) void gn_bwd_reduce_group_kernel(GnBwdArgs a, const float* __restrict__ part, int nsl,
+                                                                  int SL, float* __restrict__ nc,
+                                                                  float* __restrict__ dss, float* __restrict__ red) {
+  __shared__ double sh[3][256];
+  __shared__ float ncs[2][32];
+  const int g = blockIdx.x, n = blockIdx.y, C = a.C, cg = C / 32;
+  const int k = threadIdx.x / SL, l = threadIdx.x % SL;  // blockDim.x = cg * SL
+  const int c = g * cg + k;
   double s1 = 0, s2 = 0, s3 = 0;
-#pragma unroll 8
-  for (int s = 0; s < nsl; ++s) {
-    const float* o = part + (((int64_t)n * nsl + s) * a.C + c) * 3;
+  for (int s = l; s < nsl; s += SL) {
+    const float* o = part + (((int64_t)n * nsl + s) * C + c) * 3;
     s1 += o[0];
     s2 += o[1];
     s3 += o[2];
   }
-  const float onep = a.ss ? 1.0f + a.ss[(int64_t)n * a.ss_stride + c] : 1.0f;
-  nc[i * 3] = (float)s1;           // sum dz
-  nc[i * 3 + 1] = (float)(s1 * onep);  // sum dnrm
-  nc[i * 3 + 2] = (float)s3;       // sum dnrm xhat
-  if (dss) {  // d scale, d shift (accumulated into the emb-projection gradient)
-    dss[(int64_t)n * a.ss_stride + c] += (float)s2;
-    dss[(int64_t)n * a.ss_stride + a.C + c] += (float)s1;
+  sh[0][threadIdx.x] = s1;
+  sh[1][threadIdx.x] = s2;
+  sh[2][threadIdx.x] = s3;
+  for (int w = SL / 2; w >= 1; w >>= 1) {
+    __syncthreads();
+    if (l < w) {
+      sh[0][threadIdx.x] += sh[0][threadIdx.x + w];
+      sh[1][threadIdx.x] += sh[1][threadIdx.x + w];
+      sh[2][threadIdx.x] += sh[2][threadIdx.x + w];
+    }
+  }
+  __syncthreads();
+  if (l == 0) {
+    s1 = sh[0][threadIdx.x];
+    s2 = sh[1][threadIdx.x];
+    s3 = sh[2][threadIdx.x];
+    const int i = n * C + c;
+    const float onep = a.ss ? 1.0f + a.ss[(int64_t)n * a.ss_stride + c] : 1.0f;
+    const float v1 = (float)(s1 * onep), v2 = (float)s3;
+    nc[i * 3] = (float)s1;  // sum dz
+    nc[i * 3 + 1] = v1;     // sum dnrm
+    nc[i * 3 + 2] = v2;     // sum dnrm xhat
+    ncs[0][k] = v1;
+    ncs[1][k] = v2;
+    if (dss) {  // d scale, d shift (accumulated into the emb-projection gradient)
+      dss[(int64_t)n * a.ss_stride + c] += (float)s2;
+      dss[(int64_t)n * a.ss_stride + C + c] += (float)s1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m1 = 0, m2 = 0;
+    for (int kk = 0; kk < cg; ++kk) {
+      m1 += (double)a.gamma[g * cg + kk] * ncs[0][kk];
+      m2 += (double)a.gamma[g * cg + kk] * ncs[1][kk];
+    }
+    const double cnt = (double)cg * a.HW;
+    red[(n * 32 + g) * 2] = (float)(m1 / cnt);
+    red[(n * 32 + g) * 2 + 1] = (float)(m2 / cnt);
   }
 }
-__global__ void gn_bwd_group_kernel(GnBwdArgs a, const float* __restrict__ nc, float* __restrict__ red) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (n, g)
-  if (i >= a.N * 32) return;
-  const int n = i / 32, g = i % 32, cg = a.C / 32;
-  double m1 = 0, m2 = 0;
-  for (int k = 0; k < cg; ++k) {
-    const int c = g * cg + k;
-    m1 += (double)a.gamma[c] * nc[((int64_t)n * a.C + c) * 3 + 1];
-    m2 += (double)a.gamma[c] * nc[((int64_t)n * a.C + c) * 3 + 2];
-  }
-  const double cnt = (double)cg * a.HW;
-  red[i * 2] = (float)(m1 / cnt);
-  red[i * 2 + 1] = (float)(m2 / cnt);
+// slice lanes per channel: a power of two with cg * SL <= 256
+static int gn_reduce_lanes(int C) {
+  const int cg = C / 32;
+  int SL = 1;
+  while (2 * SL * cg <= 256) SL *= 2;
+  return SL;
 }
 __global__ void gn_bwd_param_kernel(GnBwdArgs a, const float* __restrict__ nc, float* __restrict__ dgamma,
                                     float* __restrict__ dbeta) {
@@ -2440,10 +2487,12 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
   else
     hipLaunchKernelGGL((wgrad_x3_kernel<1>), g9, b1, 0, s, a, guard, cp);
   const int64_t n = (int64_t)cout * cin * taps;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
   if (fused_db) {
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((cout + 63) / 64), dim3(64), 0, s, colpart, S, cout, db, 1);
-  } else if (db) {
+    hipLaunchKernelGGL(slab_bias_reduce_kernel, dim3(grid1(n + cout)), dim3(TB), 0, s, part, S, n, dw, colpart, cout, db);
+    return TR_LAST();
+  }
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid1(n)), dim3(TB), 0, s, part, S, n, dw, 1);
+  if (db) {
     const int64_t slice = colsum_slice(P);
     const int slices = (int)((P + slice - 1) / slice);
     if (!colpart || (int64_t)slices * cout > colpart_floats) {
@@ -2551,8 +2600,8 @@ int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x
   float* red = nc + (int64_t)N * C * 3;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gn_bwd_partial_kernel, dim3(nsl, N), dim3(256), 0, s, a, part);
-  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(grid1(N * C)), dim3(TB), 0, s, a, part, nsl, nc, dss);
-  hipLaunchKernelGGL(gn_bwd_group_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, a, nc, red);
+  const int SL = gn_reduce_lanes(C);
+  hipLaunchKernelGGL(gn_bwd_reduce_group_kernel, dim3(32, N), dim3(C / 32 * SL), 0, s, a, part, nsl, SL, nc, dss, red);
   hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
   hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl, N), dim3(256), 0, s, a, red, dx, accumulate);
   return TR_LAST();
@@ -2573,8 +2622,9 @@ int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const fl
   float* nc = work;
   float* red = nc + (int64_t)N * C * 3;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(grid1(N * C)), dim3(TB), 0, s, a, part, part_nsl, nc, dss);
-  hipLaunchKernelGGL(gn_bwd_group_kernel, dim3(grid1(N * 32)), dim3(TB), 0, s, a, nc, red);
+  const int SL = gn_reduce_lanes(C);
+  hipLaunchKernelGGL(gn_bwd_reduce_group_kernel, dim3(32, N), dim3(C / 32 * SL), 0, s, a, part, part_nsl, SL, nc, dss,
+                     red);
   hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
   hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl, N), dim3(256), 0, s, a, red, dx, accumulate);
   return TR_LAST();
