@@ -1262,7 +1262,35 @@ struct GnBwdArgs {
   const float* stats;
   // x = concat(x[C0], x1[C - C0]) (the output blocks' skip concat, read by channel range); C0 = C: one tensor
   const float* x1; int C0;
+  // optional addend of dx, [N][HW] pixels with add_stride floats each (a channel range of a wider tensor: the
+  // skip part of an output block's concat gradient, added into the encoder chain where dx is written)
+  const float* add = nullptr; int add_stride = 0;
+  // the resampling ResBlocks (rmode 1: nearest-up x2, 2: AvgPool2d(2); W = the GroupNorm input's width): dout is
+  // the gradient at the block's output resolution, read through the resample adjoint (resample4_bwd_kernel's
+  // arithmetic), and radd (optional, same resolution: the skip path's gradient) joins dx through it as well
+  int rmode = 0, W = 0;
+  const float* radd = nullptr;
 };
+// the resample adjoint of t (at the output resolution) at GroupNorm-input pixel p of image n, channels c0..c0+3
+__device__ __forceinline__ f32x4 gn_radj(const GnBwdArgs& a, const float* t, int n, int p, int c0) {
+  const int y = p / a.W, x = p - y * a.W, C = a.C;
+  f32x4 v;
+  if (a.rmode == 1) {
+    const int Ho = 2 * a.W;
+    const int64_t b0 = (((int64_t)n * Ho + 2 * y) * Ho + 2 * x) * C + c0;
+    const int64_t rs = (int64_t)Ho * C;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(t + b0), a1 = *reinterpret_cast<const f32x4*>(t + b0 + C);
+    const f32x4 a2 = *reinterpret_cast<const f32x4*>(t + b0 + rs), a3 = *reinterpret_cast<const f32x4*>(t + b0 + rs + C);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ((a0[j] + a1[j]) + a2[j]) + a3[j];
+  } else {
+    const int Ho = a.W / 2;
+    const f32x4 u = *reinterpret_cast<const f32x4*>(t + (((int64_t)n * Ho + y / 2) * Ho + x / 2) * C + c0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = u[j] / 4.0f;
+  }
+  return v;
+}
 // the thread's x quad (channels c0 .. c0 + 3 of image n): base pointer and pixel stride in its source
 __device__ __forceinline__ const float* gn_xsrc(const GnBwdArgs& a, int n, int c0, int& stride) {
   if (c0 < a.C0) {
@@ -1300,7 +1328,7 @@ __global__ __launch_bounds__(256) void gn_bwd_partial_kernel(GnBwdArgs a, float*
     const float* const xb = gn_xsrc(a, n, c0, xs);
     for (int p = p0 + r; p < p1; p += R) {
       const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + (int64_t)p * xs);
-      const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dout + base + (int64_t)p * C);
+      const f32x4 dv = a.rmode ? gn_radj(a, a.dout, n, p, c0) : *reinterpret_cast<const f32x4*>(a.dout + base + (int64_t)p * C);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float xhat = (xv[j] - mean[j]) * rstd[j];
@@ -1405,23 +1433,29 @@ static int gn_reduce_lanes(int C) {
   while (2 * SL * cg <= 256) SL *= 2;
   return SL;
 }
-__global__ void gn_bwd_param_kernel(GnBwdArgs a, const float* __restrict__ nc, float* __restrict__ dgamma,
-                                    float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.C) return;
-  double g = 0, b = 0;
-  for (int n = 0; n < a.N; ++n) {
-    b += nc[((int64_t)n * a.C + c) * 3 + 1];
-    g += nc[((int64_t)n * a.C + c) * 3 + 2];
-  }
-  dgamma[c] += (float)g;
-  dbeta[c] += (float)b;
-}
-// grid (slices, N), the (row, channel quad) layout with per-channel coefficients in registers
+// grid (nsl + ceil(C / 256), N), the (row, channel quad) layout with per-channel coefficients in registers.
+// The blocks past the nsl slices of image 0 are gn_bwd_param_kernel's (dgamma, dbeta += the image sums of nc):
+// both need only the reduce kernel's output, so the parameter gradients ride in this launch (was one more
+// launch per GroupNorm, 65 a training step).
 __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(GnBwdArgs a, const float* __restrict__ red,
-                                                        float* __restrict__ dx, int accumulate) {
+                                                        float* __restrict__ dx, int accumulate, int nsl,
+                                                        const float* __restrict__ nc, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta) {
   const int n = blockIdx.y, C = a.C;
-  const int sl = gn_sl(a.HW), p0 = blockIdx.x * sl, p1 = min(p0 + sl, a.HW);
+  if ((int)blockIdx.x >= nsl) {
+    const int c = ((int)blockIdx.x - nsl) * 256 + (int)threadIdx.x;
+    if (n != 0 || c >= C) return;
+    double g = 0, b = 0;
+#pragma unroll 8
+    for (int i = 0; i < a.N; ++i) {
+      b += nc[((int64_t)i * C + c) * 3 + 1];
+      g += nc[((int64_t)i * C + c) * 3 + 2];
+    }
+    dgamma[c] += (float)g;
+    dbeta[c] += (float)b;
+    return;
+  }
+  const int sl = (a.HW + nsl - 1) / nsl, p0 = blockIdx.x * sl, p1 = min(p0 + sl, a.HW);
   const int Q = C >> 2, R = 256 / Q;
   const int q = threadIdx.x % Q, r = threadIdx.x / Q;
   if (r >= R) return;
@@ -1446,9 +1480,11 @@ __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(GnBwdArgs a, const float
   for (int p = p0 + r; p < p1; p += R) {
     const int64_t i = base + (int64_t)p * C;
     const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + (int64_t)p * xs);
-    const f32x4 dv = *reinterpret_cast<const f32x4*>(a.dout + i);
+    const f32x4 dv = a.rmode ? gn_radj(a, a.dout, n, p, c0) : *reinterpret_cast<const f32x4*>(a.dout + i);
     f32x4 prev = {0.f, 0.f, 0.f, 0.f};
     if (accumulate) prev = *reinterpret_cast<const f32x4*>(dx + i);
+    if (a.add) prev += *reinterpret_cast<const f32x4*>(a.add + ((int64_t)n * a.HW + p) * a.add_stride + c0);
+    if (a.radd) prev += gn_radj(a, a.radd, n, p, c0);
     f32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {  // gn_bwd_partial_kernel's per-point arithmetic
@@ -1462,7 +1498,7 @@ __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(GnBwdArgs a, const float
       }
       const float dxhat = dz * onep[j] * gam[j];
       const float v = rstd[j] * (dxhat - r0[j] - xhat * r1[j]);
-      o[j] = accumulate ? prev[j] + v : v;
+      o[j] = accumulate || a.add || a.radd ? prev[j] + v : v;
     }
     *reinterpret_cast<f32x4*>(dx + i) = o;
   }
@@ -2577,24 +2613,73 @@ int ifd_tr_act_apply(const float* x, int N, int HW, int C, const float* A, const
   return launch_act_apply(x, C, N, HW, silu ? ACT_AFFINE_SILU : ACT_AFFINE, A, B, out, (hipStream_t)stream);
 }
 
+// act + nearest-up x2 of an NHWC tensor, and the raw input's nearest-up from the same read: thread = (input pixel,
+// channel quad), four 16-B stores of each (code/nn.py:92-133 after nn.py:151-152)
+__global__ __launch_bounds__(256) void act_up_kernel(const float* __restrict__ x, int C, int N, int Hin,
+                                                     const float* __restrict__ A, const float* __restrict__ B,
+                                                     float* __restrict__ out, float* __restrict__ out_raw) {
+  const int Q = C / 4, Ho = 2 * Hin;
+  const size_t tot = (size_t)N * Hin * Hin * Q;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int q = (int)(i % Q);
+  const size_t pix = i / Q;
+  const int xi = (int)(pix % Hin), yi = (int)((pix / Hin) % Hin), n = (int)(pix / ((size_t)Hin * Hin));
+  const f32x4 v = *(const f32x4*)(x + pix * C + 4 * q);
+  const f32x4 a = *(const f32x4*)(A + (size_t)n * C + 4 * q), c = *(const f32x4*)(B + (size_t)n * C + 4 * q);
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = silu_fast(a[j] * v[j] + c[j]);
+  const size_t o = (((size_t)n * Ho + 2 * yi) * Ho + 2 * xi) * C + 4 * q;
+  const size_t rs = (size_t)Ho * C;
+  *(f32x4*)(out + o) = r;
+  *(f32x4*)(out + o + C) = r;
+  *(f32x4*)(out + o + rs) = r;
+  *(f32x4*)(out + o + rs + C) = r;
+  *(f32x4*)(out_raw + o) = v;
+  *(f32x4*)(out_raw + o + C) = v;
+  *(f32x4*)(out_raw + o + rs) = v;
+  *(f32x4*)(out_raw + o + rs + C) = v;
+}
+
+int ifd_tr_act_resample(const float* x, int N, int Hin, int C, const float* A, const float* B, int mode, float* out,
+                        float* out_raw, void* stream) {
+  if (!x || !A || !B || !out || !out_raw || C % 4 || (mode != 1 && mode != 2) || (mode == 2 && Hin % 2)) {
+    set_error("ifd_tr_act_resample: bad arguments");
+    return 2;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 2) return launch_act_pool(x, C, N, Hin, ACT_AFFINE_SILU, A, B, out, out_raw, s);
+  const size_t tot = (size_t)N * Hin * Hin * (C / 4);
+  hipLaunchKernelGGL(act_up_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, x, C, N, Hin, A, B, out,
+                     out_raw);
+  return TR_LAST();
+}
+
 int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const float* gamma, const float* beta,
                   const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
                   float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream) {
   return ifd_tr_gn_bwd_cat(dout, x, C, nullptr, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, dx, accumulate,
-                           dgamma, dbeta, dss, work, work_floats, stream);
+                           dgamma, dbeta, dss, work, work_floats, nullptr, 0, stream);
 }
 
 int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
                       const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                       const float* stats, float* dx, int accumulate, float* dgamma, float* dbeta, float* dss,
-                      float* work, int64_t work_floats, void* stream) {
+                      float* work, int64_t work_floats, const float* add, int add_stride, void* stream) {
   const int nsl = gn_nsl(HW, N, C);
   const int64_t need = (int64_t)N * nsl * C * 3 + (int64_t)N * C * 3 + (int64_t)N * 64;
   if (C % 32 || C > 1024 || need > work_floats || C0 % 4 || C0 <= 0 || C0 > C || (C0 < C && !x1)) {
     set_error("ifd_tr_gn_bwd: C must be a multiple of 32 (<= 1024), 0 < C0 <= C in quads; work too small");
     return 2;
   }
+  if (add && (add_stride < C || add_stride % 4 || ((uintptr_t)add & 15))) {
+    set_error("ifd_tr_gn_bwd: addend stride must be >= C, in quads, 16-B aligned");
+    return 2;
+  }
   GnBwdArgs a{dout, x0, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, x1, C0};
+  a.add = add;
+  a.add_stride = add_stride;
   float* part = work;
   float* nc = work + (int64_t)N * nsl * C * 3;
   float* red = nc + (int64_t)N * C * 3;
@@ -2602,15 +2687,47 @@ int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x
   hipLaunchKernelGGL(gn_bwd_partial_kernel, dim3(nsl, N), dim3(256), 0, s, a, part);
   const int SL = gn_reduce_lanes(C);
   hipLaunchKernelGGL(gn_bwd_reduce_group_kernel, dim3(32, N), dim3(C / 32 * SL), 0, s, a, part, nsl, SL, nc, dss, red);
-  hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
-  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl, N), dim3(256), 0, s, a, red, dx, accumulate);
+  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl + (C + 255) / 256, N), dim3(256), 0, s, a, red, dx, accumulate, nsl, nc,
+                     dgamma, dbeta);
+  return TR_LAST();
+}
+
+int ifd_tr_gn_bwd_resampled(const float* dout, const float* x, int N, int H, int C, const float* gamma,
+                            const float* beta, int act_silu, const float* stats, int mode, const float* radd, float* dx,
+                            float* dgamma, float* dbeta, const float* add, int add_stride, float* work,
+                            int64_t work_floats, void* stream) {
+  const int HW = H * H;
+  const int nsl = gn_nsl(HW, N, C);
+  const int64_t need = (int64_t)N * nsl * C * 3 + (int64_t)N * C * 3 + (int64_t)N * 64;
+  if (C % 32 || C > 1024 || need > work_floats || (mode != 1 && mode != 2) || (mode == 2 && H % 2) ||
+      (add && (add_stride < C || add_stride % 4 || ((uintptr_t)add & 15)))) {
+    set_error("ifd_tr_gn_bwd_resampled: bad arguments or work too small");
+    return 2;
+  }
+  GnBwdArgs a{dout, x, N, HW, C, gamma, beta, nullptr, 0, act_silu, stats, nullptr, C};
+  a.add = add;
+  a.add_stride = add_stride;
+  a.rmode = mode;
+  a.W = H;
+  a.radd = radd;
+  float* part = work;
+  float* nc = work + (int64_t)N * nsl * C * 3;
+  float* red = nc + (int64_t)N * C * 3;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gn_bwd_partial_kernel, dim3(nsl, N), dim3(256), 0, s, a, part);
+  const int SL = gn_reduce_lanes(C);
+  hipLaunchKernelGGL(gn_bwd_reduce_group_kernel, dim3(32, N), dim3(C / 32 * SL), 0, s, a, part, nsl, SL, nc, nullptr,
+                     red);
+  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl + (C + 255) / 256, N), dim3(256), 0, s, a, red, dx, 0, nsl, nc,
+                     dgamma, dbeta);
   return TR_LAST();
 }
 
 int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
                             const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                             const float* stats, const float* part, int part_nsl, float* dx, int accumulate,
-                            float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream) {
+                            float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, const float* add,
+                            int add_stride, void* stream) {
   const int64_t need = (int64_t)N * C * 3 + (int64_t)N * 64;
   const int nsl = gn_nsl(HW, N, C);  // the dx pass keeps its own pixel slices
   if (C % 32 || C > 1024 || need > work_floats || C0 % 4 || C0 <= 0 || C0 > C || (C0 < C && !x1) || !part ||
@@ -2618,15 +2735,21 @@ int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const fl
     set_error("ifd_tr_gn_bwd_from_part: bad arguments or work too small");
     return 2;
   }
+  if (add && (add_stride < C || add_stride % 4 || ((uintptr_t)add & 15))) {
+    set_error("ifd_tr_gn_bwd: addend stride must be >= C, in quads, 16-B aligned");
+    return 2;
+  }
   GnBwdArgs a{dout, x0, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, x1, C0};
+  a.add = add;
+  a.add_stride = add_stride;
   float* nc = work;
   float* red = nc + (int64_t)N * C * 3;
   hipStream_t s = (hipStream_t)stream;
   const int SL = gn_reduce_lanes(C);
   hipLaunchKernelGGL(gn_bwd_reduce_group_kernel, dim3(32, N), dim3(C / 32 * SL), 0, s, a, part, part_nsl, SL, nc, dss,
                      red);
-  hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(grid1(C)), dim3(TB), 0, s, a, nc, dgamma, dbeta);
-  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl, N), dim3(256), 0, s, a, red, dx, accumulate);
+  hipLaunchKernelGGL(gn_bwd_dx_kernel, dim3(nsl + (C + 255) / 256, N), dim3(256), 0, s, a, red, dx, accumulate, nsl, nc,
+                     dgamma, dbeta);
   return TR_LAST();
 }
 

@@ -49,15 +49,18 @@ TRAIN_EXPORTS = {
     "ifd_tr_conv_wgrad_x3_gn": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp, i64, vp, i32,
                                       vp]),
     "ifd_tr_gn_bwd_cat": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, i64,
-                                vp]),
+                                vp, i32, vp]),
     "ifd_tr_gn_slices": (i64, [i32, i32, i32]),
     "ifd_tr_gnb_part_floats": (i64, [i32, i32, i32]),
     "ifd_tr_conv_x3_gnb": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp, vp, vp, vp, i32,
                                  i32, vp, i64, _c.POINTER(i32), i32, vp]),
     "ifd_tr_gn_bwd_from_part": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, i32, vp, vp,
-                                      vp, vp, i64, vp]),
+                                      vp, vp, i64, vp, i32, vp]),
     "ifd_tr_gn_coef": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, i32, f32, vp, vp, vp, vp, i64, vp]),
     "ifd_tr_act_apply": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp]),
+    "ifd_tr_act_resample": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp]),
+    "ifd_tr_gn_bwd_resampled": (i32, [vp, vp, i32, i32, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp, vp, i32, vp, i64,
+                                      vp]),
     "ifd_tr_head_x3_pack_floats": (i64, [i32]),
     "ifd_tr_conv_head_x3": (i32, [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp]),
     "ifd_tr_scale": (i32, [vp, i64, f32, vp]),
@@ -472,9 +475,18 @@ class UNetTrainer:
         chk(lib().ifd_tr_act_apply(P(x), N, HW, C, P(gn[0]), P(gn[1]), int(silu), P(out), self.s))
         return out
 
+    @staticmethod
+    def _addend(add):
+        """add = (tensor, stride, channel offset) -> (pointer, stride) for the GroupNorm backward's dx addend."""
+        if add is None:
+            return None, 0
+        t, stride, off = add
+        return _c.c_void_p(t.data_ptr() + 4 * off), stride
+
     def gn_bwd(self, dout, x, N, HW, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None, silu=True, x1=None,
-               C0=None):
-        """x1, C0: the GroupNorm input is concat(x[C0], x1[C - C0]) (read by channel range)."""
+               C0=None, add=None):
+        """x1, C0: the GroupNorm input is concat(x[C0], x1[C - C0]) (read by channel range). add = (t, stride,
+        offset): dx also gets that channel range of t (ifd_tr_gn_bwd_cat)."""
         acc = dx is not None
         if dx is None:
             dx = self._empty(N * HW * C)
@@ -485,22 +497,23 @@ class UNetTrainer:
         chk(lib().ifd_tr_gn_bwd_cat(P(dout), P(x), C0 if x1 is not None else C, P(x1), N, HW, C,
                                     P(self.p(prefix + "weight")), P(self.p(prefix + "bias")), P(ss), ss_stride,
                                     int(silu), P(stats), P(dx), int(acc), P(self.g(prefix + "weight")),
-                                    P(self.g(prefix + "bias")), P(dss), P(work), work.numel(), self.s))
+                                    P(self.g(prefix + "bias")), P(dss), P(work), work.numel(), *self._addend(add),
+                                    self.s))
         return dx
 
     def dgrad_gn_bwd(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None,
-                     silu=True, x1=None, C0=None):
+                     silu=True, x1=None, C0=None, add=None):
         """gn_bwd(conv^T(dy)) - the dgrad of conv `wname` fed into the GroupNorm backward of its input x (C
         channels; x1 / C0 as gn_bwd). On the split kernel the GroupNorm's pass 1 runs in the dgrad's epilogue
         (ifd_tr_conv_x3_gnb); shapes it does not take run conv() then gn_bwd()."""
-        out = self._dgrad_gnb(dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0)
+        out = self._dgrad_gnb(dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0, add)
         if out is not None:
             return out
         da = self.conv(dy, cdy, N, H, wname, transpose=True)
         return self.gn_bwd(da, x, N, H * H, C, prefix, stats, dx=dx, ss=ss, ss_stride=ss_stride, dss=dss, silu=silu,
-                           x1=x1, C0=C0)
+                           x1=x1, C0=C0, add=add)
 
-    def _dgrad_gnb(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0):
+    def _dgrad_gnb(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0, add=None):
         if not (self.fuse_gnb and self._x3_active(True)):
             return None
         w = self.p(wname)
@@ -531,7 +544,7 @@ class UNetTrainer:
         chk(rc)
         if nsl.value == 0:  # (the conv ran; its geometry could not carry the partial sums)
             return self.gn_bwd(da, x, N, H * H, C, prefix, stats, dx=dx, ss=ss, ss_stride=ss_stride, dss=dss,
-                               silu=silu, x1=x1, C0=C0)
+                               silu=silu, x1=x1, C0=C0, add=add)
         acc = dx is not None
         if dx is None:
             dx = self._empty(N * H * H * C)
@@ -541,7 +554,7 @@ class UNetTrainer:
         chk(lib().ifd_tr_gn_bwd_from_part(P(da), P(x), c0, P(x1), N, H * H, C, P(gam), P(bet), P(ss), ss_stride,
                                           int(silu), P(stats), P(gpart), nsl.value, P(dx), int(acc),
                                           P(self.g(prefix + "weight")), P(self.g(prefix + "bias")), P(dss), P(work),
-                                          work.numel(), self.s))
+                                          work.numel(), *self._addend(add), self.s))
         return dx
 
     def resample(self, x, N, Hin, C, mode):
@@ -668,11 +681,17 @@ class UNetTrainer:
         elif fused and not mode:  # in_layers: GroupNorm + SiLU applied by conv1's prologue (and wgrad's staging)
             g1, st1 = self.gn_coef(x, N, r * r, cin, p + "in_layers.0.")
             h1 = self.conv(x, cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias", gn=g1)
+        elif fused:  # a resampling block: act + resample of x and resample of x in one pass
+            (A, B), st1 = self.gn_coef(x, N, r * r, cin, p + "in_layers.0.")
+            a1r, xr = self._empty(N, ro, ro, cin), self._empty(N, ro, ro, cin)
+            chk(lib().ifd_tr_act_resample(P(x), N, r, cin, P(A), P(B), mode, P(a1r), P(xr), self.s))
+            h1 = self.conv(a1r, cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
         else:
             a1, st1 = self.gn_fwd(x, N, r * r, cin, p + "in_layers.0.", silu=True)
             a1r = self.resample(a1, N, r, cin, mode) if mode else a1
             h1 = self.conv(a1r, cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
-        xr = self.resample(x, N, r, cin, mode) if mode else x
+        if not (fused and mode and x1 is None):
+            xr = self.resample(x, N, r, cin, mode) if mode else x
         E = self.linear(emb, N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True)  # [N, 2 cout]
         if cin != cout:
             skip = self.conv(xr, c0, N, ro, p + "skip_connection.weight", p + "skip_connection.bias", x1=x1, c1=c1)
@@ -754,8 +773,13 @@ class UNetTrainer:
                 continue
             if section == "input":
                 break
-            for L in reversed(layers):
-                dh, r = self._layer_bwd(L, dh, N, saved, demb)
+            for i, L in enumerate(reversed(layers)):
+                # the middle block's input is the last input block's output: its first layer's dx also takes that
+                # block's skip gradient (filled by the output blocks above)
+                last = section == "middle" and i == len(layers) - 1
+                dh, r = self._layer_bwd(L, dh, N, saved, demb, add=self._skip_addend(dhs[-1]) if last else None)
+                if last:
+                    dhs[-1] = None
             if section == "output":
                 # split d cat(h, skip) (code/unet.py:170)
                 cin = layers[0]["cin"]
@@ -767,25 +791,43 @@ class UNetTrainer:
                 dhs[hs_idx] = (dh, cin, hcur, sc, N * r * r)
                 hs_idx += 1
                 dh = dprev
-        # middle block's input = the last input block's output: dh continues down the input chain
+        # middle block's input = the last input block's output: dh continues down the input chain. Input block
+        # b's output gradient = the chain's + its skip part in d cat (dhs[b]): added where block b + 1's first
+        # layer writes its dx (the GroupNorm backward's addend), else by a channel copy
         for bidx in range(len(in_blocks) - 1, -1, -1):
             section, bi, layers = in_blocks[bidx]
-            dcat, cin, off, sc, npix = dhs[bidx]
-            self.copy_ch(dcat, cin, off, dh, sc, 0, sc, npix, True)
-            for L in reversed(layers):
+            if dhs[bidx] is not None:
+                dcat, cin, off, sc, npix = dhs[bidx]
+                self.copy_ch(dcat, cin, off, dh, sc, 0, sc, npix, True)
+                dhs[bidx] = None
+            for i, L in enumerate(reversed(layers)):
+                first = i == len(layers) - 1
                 if L["kind"] == "conv_in":
                     self.wgrad(dh, L["cout"], tape["x16"], 16, N, r, L["prefix"] + "weight", L["prefix"] + "bias",
                                real_cin=L["cin"])
                     dh = None
                 else:
-                    dh, r = self._layer_bwd(L, dh, N, saved, demb)
+                    add = self._skip_addend(dhs[bidx - 1]) if first and bidx >= 1 else None
+                    dh, r = self._layer_bwd(L, dh, N, saved, demb, add=add)
+                    if add is not None:
+                        dhs[bidx - 1] = None
         # embedding MLP backward (unet.py:44-48)
         dz0 = self.linear_bwd(demb, tape["z0"], N, "time_embed.2.weight", "time_embed.2.bias", pre_silu=True)
         self.linear_bwd(dz0, tape["temb"], N, "time_embed.0.weight", "time_embed.0.bias", want_dx=False)
 
-    def _layer_bwd(self, L, dout, N, saved, demb):
+    @staticmethod
+    def _skip_addend(rec):
+        """dhs entry (d cat, its channels, skip offset, skip channels, pixels) -> gn_bwd's add = (t, stride, offset)."""
+        if rec is None:
+            return None
+        dcat, cin, off, sc, npix = rec
+        return (dcat, cin, off)
+
+    def _layer_bwd(self, L, dout, N, saved, demb, add=None):
+        """add: (t, stride, offset) added into the layer's input gradient (a ResBlock's GroupNorm dx pass)."""
         k, p = L["kind"], L["prefix"]
         if k == "attn":
+            assert add is None, "the skip addend goes to a block's first (ResBlock) layer"
             sv = saved[p]
             C = L["cin"]
             r = int(round(math.sqrt(sv["a"].shape[1])))
@@ -823,7 +865,6 @@ class UNetTrainer:
             self.wgrad(dh1, cout, sv["a1r"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
         if mode:
             da1r = self.conv(dh1, cout, N, ro, p + "in_layers.2.weight", transpose=True)
-            da1 = self.resample_bwd(da1r, N, r, cin, mode)
         if cin != cout:
             self.wgrad(dout, cout, sv["xr"], c0, N, ro, p + "skip_connection.weight", p + "skip_connection.bias",
                        x1=x1, c1=c1)
@@ -831,14 +872,22 @@ class UNetTrainer:
         else:
             dxr = dout
         if mode:
-            dx = self.gn_bwd(da1, sv["x"], N, r * r, cin, p + "in_layers.0.", sv["st1"], silu=True)
-            self.resample_bwd(dxr, N, r, cin, mode, dx=dx)
+            # GroupNorm backward through the resample adjoint: dx = gn_bwd(adj(da1r)) + adj(dxr) (+ add) in one pass
+            dx = self._empty(N * r * r * cin)
+            nsl = lib().ifd_tr_gn_slices(r * r, N, cin)
+            work = self._empty(N * nsl * cin * 3 + N * cin * 3 + N * 64)
+            ap, ast = self._addend(add)
+            pre = p + "in_layers.0."
+            chk(lib().ifd_tr_gn_bwd_resampled(P(da1r), P(sv["x"]), N, r, cin, P(self.p(pre + "weight")),
+                                              P(self.p(pre + "bias")), 1, P(sv["st1"]), mode, P(dxr), P(dx),
+                                              P(self.g(pre + "weight")), P(self.g(pre + "bias")), ap, ast, P(work),
+                                              work.numel(), self.s))
         else:
             # the skip path's gradient (dout itself, or the 1x1 conv's fresh dgrad) is the accumulation
             # target of the GroupNorm input gradient: no separate add pass; the dgrad of in_layers.2 carries
             # the GroupNorm backward's pass 1 (dgrad_gn_bwd)
             dx = self.dgrad_gn_bwd(dh1, cout, N, ro, p + "in_layers.2.weight", sv["x"], cin, p + "in_layers.0.",
-                                   sv["st1"], dx=dxr, silu=True, x1=x1, C0=c0)
+                                   sv["st1"], dx=dxr, silu=True, x1=x1, C0=c0, add=add)
         return dx, r
 
     # ------------------------------------------------------------------ loss / step

@@ -118,6 +118,11 @@ int ifd_tr_gn_coef(const float* x, int N, int HW, int C, const float* gamma, con
  * materialises a GroupNorm-applied activation when a consumer cannot apply it on load. */
 int ifd_tr_act_apply(const float* x, int N, int HW, int C, const float* A, const float* B, int silu, float* out,
                      void* stream);
+/* The resampling ResBlocks' input side in one pass (code/nn.py:189-195 with nn.py:151-152): out =
+ * resample(silu(A[n][c] x + B[n][c])) and out_raw = resample(x), mode 1 nearest-up x2, mode 2 AvgPool2d(2)
+ * (the sampler's act_pool arithmetic), at the output resolution. */
+int ifd_tr_act_resample(const float* x, int N, int Hin, int C, const float* A, const float* B, int mode, float* out,
+                        float* out_raw, void* stream);
 /* Pixel slices per image of the GroupNorm passes (ifd_tr_gn_fwd / _coef / _bwd work sizes use it): 256-pixel
  * slices, smaller on small maps so that the grid keeps >= 1024 blocks. */
 int64_t ifd_tr_gn_slices(int HW, int N, int C);
@@ -138,11 +143,21 @@ int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const
                   const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
                   float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream);
 /* ifd_tr_gn_bwd of a concat input x = concat(x0[C0], x1[C - C0]) read by channel range (the output blocks'
- * cat(h, skip), code/unet.py:170); dx is the concat's gradient as one [N][HW][C] tensor. */
+ * cat(h, skip), code/unet.py:170); dx is the concat's gradient as one [N][HW][C] tensor. add (optional, else
+ * NULL): dx also gets add[p * add_stride + c] (a channel range of a wider tensor: the skip part of an output
+ * block's concat gradient, which joins the encoder chain's gradient here instead of by a separate pass). */
 int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
                       const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                       const float* stats, float* dx, int accumulate, float* dgamma, float* dbeta, float* dss,
-                      float* work, int64_t work_floats, void* stream);
+                      float* work, int64_t work_floats, const float* add, int add_stride, void* stream);
+/* ifd_tr_gn_bwd (no scale/shift, one source) for a resampling ResBlock's in_layers GroupNorm (code/nn.py:
+ * 189-195): dout at the block's output resolution (mode 1: nearest-up x2, 2H; mode 2: AvgPool2d(2), H/2) is read
+ * through the resample adjoint, and radd (optional, same resolution: the skip path's gradient) joins dx through
+ * it too — no materialised adjoint. x: [N][H][H][C]; dx (=, at H) also gets add as ifd_tr_gn_bwd_cat. */
+int ifd_tr_gn_bwd_resampled(const float* dout, const float* x, int N, int H, int C, const float* gamma,
+                            const float* beta, int act_silu, const float* stats, int mode, const float* radd, float* dx,
+                            float* dgamma, float* dbeta, const float* add, int add_stride, float* work,
+                            int64_t work_floats, void* stream);
 /* The dgrad conv that feeds a GroupNorm backward, with that backward's pass 1 fused into its epilogue
  * (code/train_inpainting.py:15-79 backward of nn.py:46-48,151-152,203-207): out = conv^T(dy) on the split
  * kernel (ifd_tr_conv_x3_taps, 3x3, no residual), and for GroupNorm input x = concat(gx0[gc0], gx1) (cout
@@ -160,7 +175,8 @@ int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, 
 int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
                             const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                             const float* stats, const float* part, int part_nsl, float* dx, int accumulate,
-                            float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream);
+                            float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, const float* add,
+                            int add_stride, void* stream);
 /* nearest-up x2 (mode 1) / AvgPool2d(2) (mode 2) (code/nn.py:92-133) and the adjoint (dx at Hin). */
 int ifd_tr_resample(const float* x, int N, int Hin, int C, int mode, float* out, void* stream);
 int ifd_tr_resample_bwd(const float* dy, int N, int Hin, int C, int mode, float* dx, int accumulate, void* stream);

@@ -229,12 +229,12 @@ def test_conv_x3_gnb_partials_match_separate_pass(record):
                 wk = torch.empty(N * C * 3 + N * 64, device=DEV)
                 chk(lib().ifd_tr_gn_bwd_from_part(P(da), P(x0), C0, P(x1), N, H * H, C, P(gam), P(bet), P(ss),
                                                   2 * C if use_ss else 0, 1, P(st), P(gpart), nsl.value, P(dx), 0, P(dg),
-                                                  P(db), P(dss), P(wk), wk.numel(), s))
+                                                  P(db), P(dss), P(wk), wk.numel(), None, 0, s))
             else:
                 wk = torch.empty(N * nsl0 * C * 3 + N * C * 3 + N * 64, device=DEV)
                 chk(lib().ifd_tr_gn_bwd_cat(P(da), P(x0), C0, P(x1), N, H * H, C, P(gam), P(bet), P(ss),
                                             2 * C if use_ss else 0, 1, P(st), P(dx), 0, P(dg), P(db), P(dss), P(wk),
-                                            wk.numel(), s))
+                                            wk.numel(), None, 0, s))
             torch.cuda.synchronize()
             outs[fused] = (dx, dg, db, dss)
         assert int(guard.max()) == 0
@@ -327,7 +327,7 @@ def test_concat_sources_match_materialised(N, H, c0, c1, cout, record):
         work = torch.empty(N * nsl * C * 3 + N * C * 3 + N * 64, device=DEV)
         x0, cc0, x1 = (xa, c0, xb) if two else (cat, C, None)
         chk(lib().ifd_tr_gn_bwd_cat(P(da), P(x0), cc0, P(x1), N, H * H, C, P(gamma), P(beta), None, 0, 1, P(st), P(dx),
-                                    0, P(dgam), P(dbet), None, P(work), work.numel(), s))
+                                    0, P(dgam), P(dbet), None, P(work), work.numel(), None, 0, s))
         gx.append((dx, dgam, dbet))
     torch.cuda.synchronize()
     assert int(guard.max()) == 0
@@ -336,3 +336,39 @@ def test_concat_sources_match_materialised(N, H, c0, c1, cout, record):
     for a, b in zip(gx[0], gx[1]):
         assert torch.equal(a, b)
     record(f"train_fuse/concat_sources/{N}x{H}x{c0}+{c1}->{cout}", bit_identical=True)
+
+
+@pytest.mark.parametrize("N,H,C,stride,off", [(2, 16, 128, 256, 128), (3, 8, 64, 192, 64)])
+def test_gn_bwd_addend(N, H, C, stride, off):
+    """ifd_tr_gn_bwd_cat's dx addend (the output blocks' skip gradient joining the encoder chain's): dx with the
+    addend equals dx without it plus that channel range of the wider tensor, to the rounding of one add (the
+    kernel may fuse the last product and the add into one fma)."""
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, H * H, C, generator=g).to(DEV)
+    dout = torch.randn(N, H * H, C, generator=g).to(DEV)
+    wide = torch.randn(N, H * H, stride, generator=g).to(DEV)
+    gam = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    st = torch.empty(N * 64, device=DEV)
+    nsl = lib().ifd_tr_gn_slices(H * H, N, C)
+    wk = torch.empty(N * nsl * 64, device=DEV, dtype=torch.float64)
+    chk(lib().ifd_tr_gn_fwd(P(x), N, H * H, C, P(gam), P(bet), None, 0, 1, P(torch.empty_like(x)), P(st), P(wk),
+                            wk.numel(), s))
+    outs = []
+    for add in (False, True):
+        dx = torch.empty(N, H * H, C, device=DEV)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        work = torch.empty(N * nsl * C * 3 + N * C * 3 + N * 64, device=DEV)
+        ap = ctypes.c_void_p(wide.data_ptr() + 4 * off) if add else None
+        chk(lib().ifd_tr_gn_bwd_cat(P(dout), P(x), C, None, N, H * H, C, P(gam), P(bet), None, 0, 1, P(st), P(dx), 0,
+                                    P(dg), P(db), None, P(work), work.numel(), ap, stride if add else 0, s))
+        outs.append((dx, dg, db))
+    torch.cuda.synchronize()
+    ref = outs[0][0] + wide[..., off:off + C]
+    err = (outs[1][0] - ref).abs()
+    assert float(err.max()) <= 2.0 ** -22 * float(ref.abs().max()), float(err.max())
+    assert torch.equal(outs[1][1], outs[0][1]) and torch.equal(outs[1][2], outs[0][2])
