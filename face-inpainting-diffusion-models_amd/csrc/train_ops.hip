@@ -1784,6 +1784,213 @@ __global__ __launch_bounds__(256) void attn_bwd_cols_kernel(const float* __restr
   }
 }
 
+// The same backward on fp32 MFMAs (round 5; v_mfma_f32_32x32x2_f32, T = 32 KT <= 256): the VALU kernels above
+// ran the five T x T x 64 products at ~16 TFLOP/s (0.69 ms per 16x16 attention layer at B = 32).
+// Rows kernel: a block per (n, head, 128 queries), wave w takes 32 queries; K (x scale) and V in LDS as in the
+// forward (misc.hip attention_mfma_kernel). Per wave, S^T and dP^T tiles by MFMA (lane = query: its softmax,
+// rowsum(dP P) and dS = P (dP - rowsum) stay within the lane and its lane ^ 32 partner), dQ = scale (dS (k scale))
+// by MFMA, and P^T, dS^T to scratch KEY-major [n][head][key][query] (each half-wave stores 32 consecutive
+// queries of one key: coalesced). Cols kernel: a block per (n, head, 128 keys), wave w takes 32 keys; per
+// 32-query chunk the wave stages its [32 keys][32 queries] of dS^T and P^T in LDS (stride 33: the A-operand
+// reads, one key per lane, hit distinct banks) and the block the chunk's q and do rows; dK = s2 (dS^T q) and
+// dV = P^T do by MFMA. Summation orders differ from the VALU kernels (fp32 MFMA accumulation); the training
+// tests' tolerances hold (tests/test_gpu_blocks.py, tests/test_gpu_train*.py).
+constexpr int ABM_KS = 68, ABM_VS = 68;  // K / V row strides in the rows kernel (ds_read_b128 of 32 rows)
+constexpr int ABM_CS = 33;               // dS^T / P^T chunk row stride in the cols kernel
+
+template <int KT>
+__global__ __launch_bounds__(256, 1) void attn_bwd_rows_mfma_kernel(const float* __restrict__ qkv,
+                                                                   const float* __restrict__ dout, int C, float scale,
+                                                                   float* __restrict__ dqkv, float* __restrict__ Pm,
+                                                                   float* __restrict__ dSm) {
+  constexpr int T = 32 * KT;
+  extern __shared__ __attribute__((aligned(16))) float abm[];
+  float* Ks = abm;                 // [T][ABM_KS] k * scale
+  float* Vs = abm + T * ABM_KS;    // [T][ABM_VS] v
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int head = blockIdx.y, n = blockIdx.z, nh = gridDim.y;
+  const size_t rs = 3 * (size_t)C;
+  const float* base = qkv + (size_t)n * T * rs + head * 64;
+  for (int i = tid; i < T * 16; i += 256) {
+    const int row = i >> 4, c4 = 4 * (i & 15);
+    f32x4 kv = *(const f32x4*)(base + (size_t)row * rs + C + c4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) kv[j] = kv[j] * scale;
+    *(f32x4*)(Ks + row * ABM_KS + c4) = kv;
+    *(f32x4*)(Vs + row * ABM_VS + c4) = *(const f32x4*)(base + (size_t)row * rs + 2 * C + c4);
+  }
+  __syncthreads();
+  const int q0 = blockIdx.x * 128 + 32 * w;
+  if (q0 >= T) return;
+  float qv[32], dv[32];  // q (x scale) and do of query q0 + l32, channels 32 h .. 32 h + 31
+  const float* dob = dout + ((size_t)n * T + q0 + l32) * C + head * 64 + 32 * h;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const f32x4 v = *(const f32x4*)(base + (size_t)(q0 + l32) * rs + 32 * h + 4 * j);
+    const f32x4 d = *(const f32x4*)(dob + 4 * j);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      qv[4 * j + c] = v[c] * scale;
+      dv[4 * j + c] = d[c];
+    }
+  }
+  // S^T and dP^T tiles: register r of tile kt = key kt 32 + 8 (r >> 2) + 4 h + (r & 3), query q0 + l32
+  f32x16 s[KT], dp[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kt][r] = dp[kt][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 kf = *(const f32x4*)(Ks + (kt * 32 + l32) * ABM_KS + 32 * h + 4 * j);
+      const f32x4 vf = *(const f32x4*)(Vs + (kt * 32 + l32) * ABM_VS + 32 * h + 4 * j);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[c], qv[4 * j + c], s[kt], 0, 0, 0);
+        dp[kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vf[c], dv[4 * j + c], dp[kt], 0, 0, 0);
+      }
+    }
+  }
+  // softmax over the query's keys (this lane and lane ^ 32), rowsum(dP P), dS = P (dP - rowsum)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = expf(s[kt][r] - mx);
+      s[kt][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.0f / sum;
+  float dd = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[kt][r] = s[kt][r] * inv;
+      dd += dp[kt][r] * s[kt][r];
+    }
+  dd += __shfl_xor(dd, 32);
+  const size_t mo = ((size_t)n * nh + head) * T * T + q0 + l32;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dp[kt][r] = s[kt][r] * (dp[kt][r] - dd);
+      const size_t key = kt * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+      Pm[mo + key * T] = s[kt][r];
+      dSm[mo + key * T] = dp[kt][r];
+    }
+  // dQ[q][d] = scale sum_key dS[q][key] (k scale)[key][d]: A = dS (lane = query, k = the lane half's key), B = K
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o0[r] = o1[r] = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* kr = Ks + (kt * 32 + 8 * (r >> 2) + 4 * h + (r & 3)) * ABM_KS + l32;
+      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[kt][r], kr[0], o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(dp[kt][r], kr[32], o1, 0, 0, 0);
+    }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int q = q0 + 8 * (r >> 2) + 4 * h + (r & 3);
+    float* o = dqkv + ((size_t)n * T + q) * rs + head * 64 + l32;
+    o[0] = scale * o0[r];
+    o[32] = scale * o1[r];
+  }
+}
+
+template <int KT>
+__global__ __launch_bounds__(256, 1) void attn_bwd_cols_mfma_kernel(const float* __restrict__ qkv,
+                                                                   const float* __restrict__ dout, int C, float scale,
+                                                                   float* __restrict__ dqkv,
+                                                                   const float* __restrict__ Pm,
+                                                                   const float* __restrict__ dSm) {
+  constexpr int T = 32 * KT;
+  __shared__ float qs[32][64], ds_[32][64];        // the chunk's q and do rows (block)
+  __shared__ float dst[4][32 * ABM_CS], pt[4][32 * ABM_CS];  // per wave: [32 keys][32 queries] of dS^T, P^T
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int head = blockIdx.y, n = blockIdx.z, nh = gridDim.y;
+  const size_t rs = 3 * (size_t)C;
+  const float* base = qkv + (size_t)n * T * rs + head * 64;
+  const float* dob = dout + (size_t)n * T * C + head * 64;
+  const int k0 = blockIdx.x * 128 + 32 * w;
+  const bool act = k0 < T;
+  const size_t mo = ((size_t)n * nh + head) * T * T;
+  f32x16 dk0, dk1, dv0, dv1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f;
+  float* dsw = dst[w];
+  float* ptw = pt[w];
+  for (int qc = 0; qc < T; qc += 32) {
+    __syncthreads();  // the previous chunk's reads are done
+    for (int i = tid; i < 32 * 16; i += 256) {
+      const int row = i >> 4, c4 = 4 * (i & 15);
+      *(f32x4*)&qs[row][c4] = *(const f32x4*)(base + (size_t)(qc + row) * rs + c4);
+      *(f32x4*)&ds_[row][c4] = *(const f32x4*)(dob + (size_t)(qc + row) * C + c4);
+    }
+    if (act) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int idx = e * 64 + lane, row = idx >> 3, c4 = 4 * (idx & 7);
+        const size_t g = mo + (size_t)(k0 + row) * T + qc + c4;
+        const f32x4 a = *(const f32x4*)(dSm + g), b = *(const f32x4*)(Pm + g);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          dsw[row * ABM_CS + c4 + c] = a[c];
+          ptw[row * ABM_CS + c4 + c] = b[c];
+        }
+      }
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int qq = 2 * kk + h;  // this lane half's query of the step
+        const float a_ds = dsw[l32 * ABM_CS + qq], a_p = ptw[l32 * ABM_CS + qq];
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_ds, qs[qq][l32], dk0, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_ds, qs[qq][l32 + 32], dk1, 0, 0, 0);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_p, ds_[qq][l32], dv0, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a_p, ds_[qq][l32 + 32], dv1, 0, 0, 0);
+      }
+    }
+  }
+  if (!act) return;
+  const float s2 = scale * scale;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int key = k0 + 8 * (r >> 2) + 4 * h + (r & 3);
+    float* o = dqkv + ((size_t)n * T + key) * rs + head * 64 + l32;
+    o[C] = s2 * dk0[r];
+    o[C + 32] = s2 * dk1[r];
+    o[2 * C] = dv0[r];
+    o[2 * C + 32] = dv1[r];
+  }
+}
+
+template <int KT>
+static void launch_attn_bwd_mfma(const float* qkv, const float* dout, int N, int C, float scale, float* dqkv, float* Pm,
+                                 float* dSm, hipStream_t s) {
+  constexpr int T = 32 * KT;
+  const size_t lds = (size_t)T * (ABM_KS + ABM_VS) * sizeof(float);
+  static bool attr[kMaxDevices] = {};
+  (void)set_lds_attr_once(attr, reinterpret_cast<const void*>(&attn_bwd_rows_mfma_kernel<KT>), (int)lds);
+  dim3 g((T + 127) / 128, C / 64, N);
+  hipLaunchKernelGGL(attn_bwd_rows_mfma_kernel<KT>, g, dim3(256), lds, s, qkv, dout, C, scale, dqkv, Pm, dSm);
+  hipLaunchKernelGGL(attn_bwd_cols_mfma_kernel<KT>, g, dim3(256), 0, s, qkv, dout, C, scale, dqkv, Pm, dSm);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Linear layers of the embedding path (code/unet.py:44-48, code/nn.py:167-170): y = pre(x) W^T + b,
 // W [N][K] (torch), pre = identity | SiLU. M (the batch) is small; one thread per output.
@@ -2815,6 +3022,14 @@ int ifd_tr_attention_bwd(const float* qkv, const float* dout, int N, int T, int 
   }
   float* Pm = scratch;
   float* dS = scratch + (int64_t)N * nh * T * T;
+  hipStream_t s = (hipStream_t)stream;
+  if (T == 256 || T == 128 || T == 64 || T == 32) {  // the MFMA kernels (the VALU ones for other T)
+    if (T == 256) launch_attn_bwd_mfma<8>(qkv, dout, N, C, scale, dqkv, Pm, dS, s);
+    if (T == 128) launch_attn_bwd_mfma<4>(qkv, dout, N, C, scale, dqkv, Pm, dS, s);
+    if (T == 64) launch_attn_bwd_mfma<2>(qkv, dout, N, C, scale, dqkv, Pm, dS, s);
+    if (T == 32) launch_attn_bwd_mfma<1>(qkv, dout, N, C, scale, dqkv, Pm, dS, s);
+    return TR_LAST();
+  }
   dim3 g((T + AB_R - 1) / AB_R, nh, N);
   const size_t lds = ((size_t)2 * AB_R * T + 2 * AB_R * 64) * sizeof(float);
   if (lds > 160 * 1024) {
@@ -2823,7 +3038,6 @@ int ifd_tr_attention_bwd(const float* qkv, const float* dout, int N, int T, int 
   }
   static bool attr[kMaxDevices] = {};
   (void)set_lds_attr_once(attr, reinterpret_cast<const void*>(&attn_bwd_rows_kernel), (int)lds);
-  hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(attn_bwd_rows_kernel, g, dim3(256), lds, s, qkv, dout, T, C, scale, dqkv, Pm, dS);
   hipLaunchKernelGGL(attn_bwd_cols_kernel, g, dim3(256), 0, s, qkv, dout, T, C, scale, dqkv, Pm, dS);
   return TR_LAST();
