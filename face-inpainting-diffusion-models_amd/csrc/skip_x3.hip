@@ -15,8 +15,8 @@
 // independently (no further barrier): wave w walks 32-pixel tiles; per k = 16 step its lane (h, l32)
 // loads channels 16 ks + 8 h .. + 7 of tile pixel l32 (two 16-B loads, SK_D steps ahead in a
 // register ring that runs on across tiles), splits them in registers, reads the B fragments from
-// LDS and issues 3 x NTC / 32 MFMAs. Epilogue: x 2^-11 + bias, dword stores (two 128-B row segments
-// per instruction).
+// LDS and issues 3 x NTC / 32 MFMAs. Epilogue: x 2^-11 + bias, quad-transposed dwordx4 stores (8 pixels x
+// 128 B per instruction).
 #include "conv.h"
 #include "conv_dev.h"
 
@@ -42,6 +42,8 @@ constexpr int SK_D = SK_DEPTH;  // k steps of operand in flight per wave
 #define SK_WPE 2  // waves per SIMD the registers are budgeted for (blocks per CU = SK_WPE / 2)
 #endif
 constexpr int SK_LDS_MAX = SK_LDS_KB * 1024;
+
+
 constexpr float kScale = 2048.0f;  // 2^11
 
 // hi = f16(v) for the pair (one v_cvt_pk_f16_f32), lo = f16(v - hi) (v_fma_mix: v - hi exact in
@@ -188,16 +190,43 @@ __global__ __launch_bounds__(SK_NT, SK_WPE) void skip_x3_kernel(Skip1x1Params p)
       }
     }
     // epilogue: register (nr, r) of lane (h, l32) = channel nt NTC + 32 nr + l32 of tile pixel
-    // 8 (r >> 2) + 4 h + (r & 3)
-    const rsrc_t ro = mkrsrc(p.out + (size_t)t * 32 * p.cout);
-    const int vb = ((4 * h) * p.cout + nt * NTC + l32) * 4;
+    // 8 (r >> 2) + 4 h + (r & 3). Per (nr, g) the quad's 4 lanes (channels 4a .. 4a + 3 of the 32-block) x
+    // registers 4g .. 4g + 3 (pixels 8 g + 4 h + 0..3) are transposed by two DPP butterflies, so lane 4a + i holds
+    // pixel 8 g + 4 h + i's four channels: one dwordx4 store per (nr, g) writes 8 pixels x 128 B. (Round 5: was
+    // 64 dword stores per lane and tile; timing ablations put the stores at ~44 % of this memory-bound kernel,
+    // and the wide stores take the 256^2 layer 0.675 -> 0.657 ms per eval, profiles/r05i.)
+    const int qi = l32 & 3;
+    const int vb4 = ((4 * h + qi) * p.cout + nt * NTC + (l32 & ~3)) * 4;
 #pragma unroll
     for (int nr = 0; nr < NR; ++nr) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float x = (acc[nr][r] + accl[nr][r]) * (1.0f / kScale) + bias[nr];
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), ro, vb + nr * 128,
-                                              (8 * (r >> 2) + (r & 3)) * p.cout * 4, 0);
+      for (int g = 0; g < 4; ++g) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (acc[nr][4 * g + j] + accl[nr][4 * g + j]) * (1.0f / kScale) + bias[nr];
+        // stage 1 (lane ^ 1, registers ^ 1), stage 2 (lane ^ 2, registers ^ 2): v[j] of lane i -> lane j's v[i]
+#define SK_QP(x, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), ctrl, 0xf, 0xf, false))
+        {
+          const float t0 = SK_QP(v[0], 0xB1), t1 = SK_QP(v[1], 0xB1);  // quad_perm [1,0,3,2]
+          const float t2 = SK_QP(v[2], 0xB1), t3 = SK_QP(v[3], 0xB1);
+          const bool odd = qi & 1;
+          v[0] = odd ? t1 : v[0];
+          v[1] = odd ? v[1] : t0;
+          v[2] = odd ? t3 : v[2];
+          v[3] = odd ? v[3] : t2;
+        }
+        {
+          const float t0 = SK_QP(v[0], 0x4E), t1 = SK_QP(v[1], 0x4E);  // quad_perm [2,3,0,1]
+          const float t2 = SK_QP(v[2], 0x4E), t3 = SK_QP(v[3], 0x4E);
+          const bool hi = qi & 2;
+          v[0] = hi ? t2 : v[0];
+          v[1] = hi ? t3 : v[1];
+          v[2] = hi ? v[2] : t0;
+          v[3] = hi ? v[3] : t1;
+        }
+#undef SK_QP
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}), ro,
+                                               vb4 + nr * 128, 8 * g * p.cout * 4, 0);
       }
     }
   }
