@@ -195,6 +195,7 @@ __global__ __launch_bounds__(SK_NT, SK_WPE) void skip_x3_kernel(Skip1x1Params p)
     // pixel 8 g + 4 h + i's four channels: one dwordx4 store per (nr, g) writes 8 pixels x 128 B. (Round 5: was
     // 64 dword stores per lane and tile; timing ablations put the stores at ~44 % of this memory-bound kernel,
     // and the wide stores take the 256^2 layer 0.675 -> 0.657 ms per eval, profiles/r05i.)
+    const rsrc_t ro = mkrsrc(p.out + (size_t)t * 32 * p.cout);
     const int qi = l32 & 3;
     const int vb4 = ((4 * h + qi) * p.cout + nt * NTC + (l32 & ~3)) * 4;
 #pragma unroll
