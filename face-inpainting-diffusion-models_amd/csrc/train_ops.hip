@@ -2203,13 +2203,10 @@ __global__ void adamw_kernel(float* __restrict__ p, float* __restrict__ g, float
 
 // 3xf16 split packing of a 3x3 conv weight on the device (unet.hip pack_conv_x3's layout and
 // arithmetic): one thread per (ct, chunk, tap, h, col, j) writes both parts.
-__global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int cin, int cin_pad16, int cout_pad,
-                                    int transpose, _Float16* __restrict__ dst, unsigned* guard) {
+__device__ __forceinline__ void pack3x3_elem(const float* __restrict__ w, int cout, int cin, int cin_pad16,
+                                             int transpose, _Float16* __restrict__ dst, unsigned* guard, int64_t i) {
 #pragma clang fp contract(off)
   const int nch = cin_pad16 / 16;
-  const int64_t tot = (int64_t)(cout_pad / 64) * nch * 9 * 2 * 64 * 8;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= tot) return;
   const int j = (int)(i & 7);
   int64_t r = i >> 3;
   const int col = (int)(r & 63);
@@ -2235,17 +2232,22 @@ __global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int c
   dst[((base + hh) * 64 + col) * 8 + j] = (_Float16)s;
   dst[((base + 2 + hh) * 64 + col) * 8 + j] = lo;
 }
+__device__ __forceinline__ int64_t pack3x3_count(int cin_pad16, int cout_pad) {
+  return (int64_t)(cout_pad / 64) * (cin_pad16 / 16) * 9 * 2 * 64 * 8;
+}
+__global__ void pack_conv_x3_kernel(const float* __restrict__ w, int cout, int cin, int cin_pad16, int cout_pad,
+                                    int transpose, _Float16* __restrict__ dst, unsigned* guard) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < pack3x3_count(cin_pad16, cout_pad)) pack3x3_elem(w, cout, cin, cin_pad16, transpose, dst, guard, i);
+}
 
 // 3xf16 packing of a 1x1 conv weight for the split kernel's 1x1 chunks (unet.hip pack_skip_x3's layout:
 // [cout_pad/64][cin/32][q][part][h][64][8] f16, element (q, part, h, col, j) of chunk s = split part of
 // W[64 ct + col][32 s + 16 h + 8 q + j]); transpose=1 packs the dgrad conv (out = cin, in = cout).
-__global__ void pack_conv1x1_x3_kernel(const float* __restrict__ w, int cout, int cin, int cs_pad, int cout_pad,
-                                       int transpose, _Float16* __restrict__ dst, unsigned* guard) {
+__device__ __forceinline__ void pack1x1_elem(const float* __restrict__ w, int cout, int cin, int cs_pad,
+                                             int transpose, _Float16* __restrict__ dst, unsigned* guard, int64_t i) {
 #pragma clang fp contract(off)
   const int ns = cs_pad / 32;
-  const int64_t tot = (int64_t)(cout_pad / 64) * ns * 2 * 2 * 64 * 8;  // without the part index
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= tot) return;
   const int j = (int)(i & 7);
   int64_t r = i >> 3;
   const int col = (int)(r & 63);
@@ -2270,6 +2272,40 @@ __global__ void pack_conv1x1_x3_kernel(const float* __restrict__ w, int cout, in
   const size_t base = ((((size_t)ct * ns + sk) * 2 + qq) * 2) * 2;  // [ct][s][q][part][h]
   dst[((base + 0 + hh) * 64 + col) * 8 + j] = (_Float16)sc;
   dst[((base + 2 + hh) * 64 + col) * 8 + j] = lo;
+}
+__device__ __forceinline__ int64_t pack1x1_count(int cs_pad, int cout_pad) {
+  return (int64_t)(cout_pad / 64) * (cs_pad / 32) * 2 * 2 * 64 * 8;  // without the part index
+}
+__global__ void pack_conv1x1_x3_kernel(const float* __restrict__ w, int cout, int cin, int cs_pad, int cout_pad,
+                                       int transpose, _Float16* __restrict__ dst, unsigned* guard) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < pack1x1_count(cs_pad, cout_pad)) pack1x1_elem(w, cout, cin, cs_pad, transpose, dst, guard, i);
+}
+
+// Every split-kernel weight packing of a training step in one launch (round 5; was one launch per conv and
+// direction, ~170 a step). Descriptor table (device, built once by the caller): a block's descriptor is found
+// by a binary search over the block offsets (uniform per block), then each thread packs one element as the
+// single-conv kernels do.
+struct PackDesc {
+  const float* w;
+  void* dst;
+  int cout, cin, pad, cout_pad, transpose, taps;
+  int64_t block0;  // first block of this descriptor
+};
+__global__ void pack_x3_batch_kernel(const PackDesc* __restrict__ d, int nd, unsigned* guard) {
+  const int64_t b = blockIdx.x;
+  int lo = 0, hi = nd - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].block0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const PackDesc e = d[lo];
+  const int64_t i = (b - e.block0) * blockDim.x + threadIdx.x;
+  if (e.taps == 9) {
+    if (i < pack3x3_count(e.pad, e.cout_pad)) pack3x3_elem(e.w, e.cout, e.cin, e.pad, e.transpose, (_Float16*)e.dst, guard, i);
+  } else {
+    if (i < pack1x1_count(e.pad, e.cout_pad)) pack1x1_elem(e.w, e.cout, e.cin, e.pad, e.transpose, (_Float16*)e.dst, guard, i);
+  }
 }
 
 __global__ void scale_kernel(float* __restrict__ x, int64_t n, float s) {
@@ -2412,6 +2448,18 @@ int ifd_tr_pack_conv_x3(const float* w, int cout, int cin, int taps, int cin_pad
   const int64_t tot = (int64_t)(cout_pad / 64) * (cin_pad16 / 16) * 9 * 2 * 64 * 8;
   hipLaunchKernelGGL(pack_conv_x3_kernel, dim3(grid1(tot)), dim3(TB), 0, (hipStream_t)stream, w, cout, cin, cin_pad16,
                      cout_pad, transpose, (_Float16*)wx3, guard);
+  return TR_LAST();
+}
+
+int64_t ifd_tr_pack_desc_bytes() { return (int64_t)sizeof(PackDesc); }
+
+int ifd_tr_pack_x3_batch(const void* desc, int ndesc, int64_t nblocks, unsigned* guard, void* stream) {
+  if (!desc || ndesc <= 0 || nblocks <= 0 || !guard) {
+    set_error("ifd_tr_pack_x3_batch: bad arguments");
+    return 2;
+  }
+  hipLaunchKernelGGL(pack_x3_batch_kernel, dim3((unsigned)nblocks), dim3(TB), 0, (hipStream_t)stream,
+                     (const PackDesc*)desc, ndesc, guard);
   return TR_LAST();
 }
 

@@ -35,6 +35,8 @@ TRAIN_EXPORTS = {
     "ifd_tr_pack_conv": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
     "ifd_tr_conv_part_floats": (i64, [i32, i32, i32, i32, i32, i32, i32]),
     "ifd_tr_pack_conv_x3": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "ifd_tr_pack_desc_bytes": (i64, []),
+    "ifd_tr_pack_x3_batch": (i32, [vp, i32, i64, vp, vp]),
     "ifd_tr_conv_x3_part_floats": (i64, [i32, i32, i32, i32]),
     "ifd_tr_conv_x3": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, vp]),
     "ifd_tr_conv_x3_taps": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, i32, vp]),
@@ -187,6 +189,10 @@ class UNetTrainer:
         self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
         self._grad_clean = False
         self._pack_cache = {}
+        # the split kernels' packed weights, kept across steps: every step re-packs them all in one launch at
+        # the start of the forward (_repack_all); a pack first needed mid-step is packed alone and joins the table
+        self._pack_persist = {}
+        self._pack_table = None
         # GroupNorm granule statistics of forward activations, keyed by data_ptr: (tensor, stats, E, cnt,
         # channels, second-source stats). Valid only while the tensor holds what its producing conv wrote:
         # the `is` check guards against a reused address, and every in-place write to a tensor (the
@@ -245,6 +251,44 @@ class UNetTrainer:
             self._pack_cache[key] = buf
         return buf, pout, pin, taps, bn, cin_pad, cout_pad
 
+    def _x3_pack(self, name, cout, cin, taps, pad, cout_pad, transpose):
+        """The split kernel's packing of conv weight `name` (ifd_tr_pack_conv_x3) in a buffer kept across steps."""
+        key = (name, int(transpose), taps, pad, cout_pad)
+        buf = self._pack_persist.get(key)
+        if buf is None:
+            buf = self._empty(cout_pad * pad * taps)
+            self._pack_persist[key] = buf
+            self._pack_table = None
+        chk(lib().ifd_tr_pack_conv_x3(P(self.p(name)), cout, cin, taps, pad, cout_pad, int(transpose), P(buf),
+                                      P(self._guard), self.s))
+        return buf
+
+    _PACK_DESC = np.dtype([("w", "<u8"), ("dst", "<u8"), ("cout", "<i4"), ("cin", "<i4"), ("pad", "<i4"),
+                           ("cout_pad", "<i4"), ("transpose", "<i4"), ("taps", "<i4"), ("block0", "<i8")])
+
+    def _repack_all(self):
+        """Start of a forward: this step's weights into every kept split-kernel packing, one launch
+        (ifd_tr_pack_x3_batch; was ~170 launches a step). The forward's lookups then find them packed."""
+        self._pack_cache = {}
+        if not (self._pack_persist and self._split()):
+            return
+        if self._pack_table is None:
+            assert lib().ifd_tr_pack_desc_bytes() == self._PACK_DESC.itemsize
+            recs = np.zeros(len(self._pack_persist), dtype=self._PACK_DESC)
+            nb = 0
+            for i, ((name, tr, taps, pad, cout_pad), buf) in enumerate(self._pack_persist.items()):
+                w = self.p(name)
+                cout, cin = w.shape[0], w.shape[1]
+                n = (cout_pad // 64) * (pad // 16) * 9 * 2 * 64 * 8 if taps == 9 else \
+                    (cout_pad // 64) * (pad // 32) * 2 * 2 * 64 * 8
+                recs[i] = (w.data_ptr(), buf.data_ptr(), cout, cin, pad, cout_pad, tr, taps, nb)
+                nb += (n + 255) // 256
+            self._pack_table = (torch.from_numpy(recs.view(np.uint8)).to(self.dev), len(recs), nb)
+        t, n, nb = self._pack_table
+        chk(lib().ifd_tr_pack_x3_batch(P(t), n, nb, P(self._guard), self.s))
+        for (name, tr, taps, pad, cout_pad), buf in self._pack_persist.items():
+            self._pack_cache[(name, tr, "x3")] = buf
+
     def _split(self):
         return self.precision in self.SPLIT_MODES
 
@@ -281,9 +325,7 @@ class UNetTrainer:
         key = (name, int(transpose), "x3")
         wx3 = self._pack_cache.get(key)
         if wx3 is None:
-            wx3 = self._empty(ppad * cin_pad * taps)
-            chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, taps, cin_pad, ppad, int(transpose), P(wx3),
-                                          P(self._guard), self.s))
+            wx3 = self._x3_pack(name, cout, cin, taps, cin_pad, ppad, transpose)
             self._pack_cache[key] = wx3
         b = self.p(bias_name) if bias_name else self._zero_bias
         out = self._empty(N, H, H, ppad)
@@ -525,8 +567,7 @@ class UNetTrainer:
         key = (wname, 1, "x3")
         wx3 = self._pack_cache.get(key)
         if wx3 is None:
-            wx3 = self._empty(cin * cdy * 9)
-            chk(lib().ifd_tr_pack_conv_x3(P(w), cout, cin, 9, cdy, cin, 1, P(wx3), P(self._guard), self.s))
+            wx3 = self._x3_pack(wname, cout, cin, 9, cdy, cin, 1)
             self._pack_cache[key] = wx3
         da = self._empty(N, H, H, cin)
         pf = lib().ifd_tr_conv_x3_part_floats(N, H, cdy, cin)
@@ -602,9 +643,9 @@ class UNetTrainer:
         x, masked_image [N,3,H,W], mask [N,1,H,W] NCHW fp32; t int64 [N]. Returns out6 NHWC [N,H,W,6]."""
         cfg = self.cfg
         N, _, H, _ = x.shape
-        self._pack_cache = {}
         self._gstat = {}
         self.s = _lib.stream_ptr(self.dev)
+        self._repack_all()
         tape = {"N": N, "H": H}
         # time embedding: temb -> Linear -> SiLU -> Linear (unet.py:44-48); all emb_layers (nn.py:167-170)
         temb = self._empty(N, cfg.model_channels)
@@ -1020,6 +1061,8 @@ class BlockTrainer(UNetTrainer):
         self._guard = torch.zeros(4, device=self.dev, dtype=torch.int32)
         self._grad_clean = False
         self._pack_cache = {}
+        self._pack_persist = {}
+        self._pack_table = None
         self._gstat = {}
         self.s = None
 
