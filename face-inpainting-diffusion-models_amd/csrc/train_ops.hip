@@ -2284,15 +2284,16 @@ __global__ void pack_conv1x1_x3_kernel(const float* __restrict__ w, int cout, in
 
 // Every split-kernel weight packing of a training step in one launch (round 5; was one launch per conv and
 // direction, ~170 a step). Descriptor table (device, built once by the caller): a block's descriptor is found
-// by a binary search over the block offsets (uniform per block), then each thread packs one element as the
-// single-conv kernels do.
+// by a binary search over the block offsets (uniform per block), then each thread packs PK_EPT elements
+// (256 apart) as the single-conv kernels do.
 struct PackDesc {
   const float* w;
   void* dst;
   int cout, cin, pad, cout_pad, transpose, taps;
   int64_t block0;  // first block of this descriptor
 };
-__global__ void pack_x3_batch_kernel(const PackDesc* __restrict__ d, int nd, unsigned* guard) {
+constexpr int PK_EPT = 32;  // elements per thread of the batched packing (amortises the descriptor search)
+__global__ __launch_bounds__(256) void pack_x3_batch_kernel(const PackDesc* __restrict__ d, int nd, unsigned* guard) {
   const int64_t b = blockIdx.x;
   int lo = 0, hi = nd - 1;
   while (lo < hi) {
@@ -2300,11 +2301,19 @@ __global__ void pack_x3_batch_kernel(const PackDesc* __restrict__ d, int nd, uns
     if (d[mid].block0 <= b) lo = mid; else hi = mid - 1;
   }
   const PackDesc e = d[lo];
-  const int64_t i = (b - e.block0) * blockDim.x + threadIdx.x;
+  const int64_t i0 = (b - e.block0) * 256 * PK_EPT + threadIdx.x;
   if (e.taps == 9) {
-    if (i < pack3x3_count(e.pad, e.cout_pad)) pack3x3_elem(e.w, e.cout, e.cin, e.pad, e.transpose, (_Float16*)e.dst, guard, i);
+    const int64_t n = pack3x3_count(e.pad, e.cout_pad);
+    for (int k = 0; k < PK_EPT; ++k) {
+      const int64_t i = i0 + 256 * k;
+      if (i < n) pack3x3_elem(e.w, e.cout, e.cin, e.pad, e.transpose, (_Float16*)e.dst, guard, i);
+    }
   } else {
-    if (i < pack1x1_count(e.pad, e.cout_pad)) pack1x1_elem(e.w, e.cout, e.cin, e.pad, e.transpose, (_Float16*)e.dst, guard, i);
+    const int64_t n = pack1x1_count(e.pad, e.cout_pad);
+    for (int k = 0; k < PK_EPT; ++k) {
+      const int64_t i = i0 + 256 * k;
+      if (i < n) pack1x1_elem(e.w, e.cout, e.cin, e.pad, e.transpose, (_Float16*)e.dst, guard, i);
+    }
   }
 }
 

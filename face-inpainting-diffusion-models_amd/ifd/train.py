@@ -282,7 +282,7 @@ class UNetTrainer:
                 n = (cout_pad // 64) * (pad // 16) * 9 * 2 * 64 * 8 if taps == 9 else \
                     (cout_pad // 64) * (pad // 32) * 2 * 2 * 64 * 8
                 recs[i] = (w.data_ptr(), buf.data_ptr(), cout, cin, pad, cout_pad, tr, taps, nb)
-                nb += (n + 255) // 256
+                nb += (n + 8191) // 8192  # 256 threads x 32 elements per block (ifd_train.h)
             self._pack_table = (torch.from_numpy(recs.view(np.uint8)).to(self.dev), len(recs), nb)
         t, n, nb = self._pack_table
         chk(lib().ifd_tr_pack_x3_batch(P(t), n, nb, P(self._guard), self.s))

@@ -46,7 +46,7 @@ int ifd_tr_pack_conv_x3(const float* w, int cout, int cin, int taps, int cin_pad
 /* Every ifd_tr_pack_conv_x3 of a step in one launch: desc = a device array of ndesc records (ifd_tr_pack_desc_bytes
  * bytes each: const float* w; void* dst; int cout, cin, pad (cin_pad16 or the 1x1 operand's channel pad),
  * cout_pad, transpose, taps; int64 first block), in block order, each record's blocks = ceil(packed f16 pairs /
- * 256); nblocks = the total. */
+ * 8192) (256 threads x 32 elements); nblocks = the total. */
 int64_t ifd_tr_pack_desc_bytes(void);
 int ifd_tr_pack_x3_batch(const void* desc, int ndesc, int64_t nblocks, unsigned* guard, void* stream);
 int64_t ifd_tr_conv_x3_part_floats(int N, int H, int cin_pad, int cout);
