@@ -554,6 +554,8 @@ int conv_pick_bn(int cout, int taps, int H, int W, int N) {
 // Tile geometry + split-K. BM = 256 (8 rows x 32 columns of one image) where the layer is wide and
 // the grid still gives >= 2 blocks per CU: it halves the weight-slab loads per MFMA, the producer's
 // bottleneck. Otherwise BM = 128, with split-K to cover the chip on the low-resolution layers.
+constexpr long kInvBatch = 16;  // the batch-invariant geometry's reference batch (the bench's images per GPU)
+
 void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool x3) {
   const bool allow256 = !p.opt_bm128;  // (the training 1x1 convs: 256-pixel tiles are instantiated for 3x3 only)
   int bm = 128;
@@ -563,7 +565,7 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
     if (bn == 64 && W >= 16 && H >= 256 / (W < 32 ? W : 32)) bm = 256;
     if (bn == 64 && W == 8 && H == 8 && N % 4 == 0 && !p.opt_invariant) bm = 256;  // four whole 8 x 8 images per tile
   } else if (allow256 && bn == 64 && W >= 32 && H >= 8) {
-    const long blocks256 = (long)(p.opt_invariant ? 1 : N) * (H / 8) * (W / 32) * (p.cout_pad / bn);
+    const long blocks256 = (long)(p.opt_invariant ? kInvBatch : N) * (H / 8) * (W / 32) * (p.cout_pad / bn);
     if (blocks256 >= 512) bm = 256;
   }
   p.bm = bm;
@@ -576,8 +578,10 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
   p.lg_tpi = __builtin_ctz(p.TH * p.TW);
   const int tiles_n = (N + p.IMGS - 1) / p.IMGS;
   p.npix_tiles = tiles_n * p.tiles_y * p.tiles_x;
-  // batch-invariant option: split as if the launch held one image (tile row) only
-  const long blocks = (long)(p.opt_invariant ? (p.npix_tiles / tiles_n) : p.npix_tiles) * (p.cout_pad / bn);
+  // batch-invariant option: the geometry of a fixed reference batch (kInvBatch images), whatever the launch
+  // holds, so an image's arithmetic (split-K factor, tile shape) does not depend on its batch (round 5: was one
+  // image, which over-split the bench's 16- and 64-image launches: 13-14 % slower, profiles/r05b)
+  const long blocks = (long)(p.opt_invariant ? (p.npix_tiles / tiles_n) * kInvBatch : p.npix_tiles) * (p.cout_pad / bn);
   int S = 1;
   if (x3 && bm == 256) {
     // persistent units: split K until the units cover the 256 CUs, keeping >= 4 chunks per unit
