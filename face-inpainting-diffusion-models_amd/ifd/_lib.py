@@ -132,7 +132,8 @@ def ptr(t):
     """Raw device pointer of a contiguous fp32/int64 tensor (None -> NULL)."""
     if t is None:
         return None
-    assert t.is_contiguous(), "ifd: tensors must be contiguous"
+    if not t.is_contiguous():  # (a raise, not an assert: python -O must not hand a strided tensor to the library)
+        raise ValueError("ifd: tensors must be contiguous")
     return ctypes.c_void_p(t.data_ptr())
 
 

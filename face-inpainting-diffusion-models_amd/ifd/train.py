@@ -273,7 +273,8 @@ class UNetTrainer:
         if not (self._pack_persist and self._split()):
             return
         if self._pack_table is None:
-            assert lib().ifd_tr_pack_desc_bytes() == self._PACK_DESC.itemsize
+            if lib().ifd_tr_pack_desc_bytes() != self._PACK_DESC.itemsize:  # (not an assert: kept under python -O)
+                raise RuntimeError("ifd_tr_pack_x3_batch descriptor layout differs from train.py's _PACK_DESC")
             recs = np.zeros(len(self._pack_persist), dtype=self._PACK_DESC)
             nb = 0
             for i, ((name, tr, taps, pad, cout_pad), buf) in enumerate(self._pack_persist.items()):
@@ -868,7 +869,8 @@ class UNetTrainer:
         """add: (t, stride, offset) added into the layer's input gradient (a ResBlock's GroupNorm dx pass)."""
         k, p = L["kind"], L["prefix"]
         if k == "attn":
-            assert add is None, "the skip addend goes to a block's first (ResBlock) layer"
+            if add is not None:
+                raise ValueError("the skip addend goes to a block's first (ResBlock) layer")
             sv = saved[p]
             C = L["cin"]
             r = int(round(math.sqrt(sv["a"].shape[1])))
