@@ -563,7 +563,9 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
     // 3xf16 split kernel (conv_x3.hip): 256-pixel tiles of one image (8 x 32 or 16 x 16) whatever
     // the tile count (persistent grid); nchunks = 16-channel chunks of the whole K stream
     if (bn == 64 && W >= 16 && H >= 256 / (W < 32 ? W : 32)) bm = 256;
-    if (bn == 64 && W == 8 && H == 8 && N % 4 == 0 && !p.opt_invariant) bm = 256;  // four whole 8 x 8 images per tile
+    // four whole 8 x 8 images per tile; the batch-invariant geometry takes them at any N (a partial last tile
+    // recomputes the batch's last image in its spare slots, conv_x3.hip unit_of)
+    if (bn == 64 && W == 8 && H == 8 && (N % 4 == 0 || p.opt_invariant)) bm = 256;
   } else if (allow256 && bn == 64 && W >= 32 && H >= 8) {
     const long blocks256 = (long)(p.opt_invariant ? kInvBatch : N) * (H / 8) * (W / 32) * (p.cout_pad / bn);
     if (blocks256 >= 512) bm = 256;
@@ -581,7 +583,8 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
   // batch-invariant option: the geometry of a fixed reference batch (kInvBatch images), whatever the launch
   // holds, so an image's arithmetic (split-K factor, tile shape) does not depend on its batch (round 5: was one
   // image, which over-split the bench's 16- and 64-image launches: 13-14 % slower, profiles/r05b)
-  const long blocks = (long)(p.opt_invariant ? (p.npix_tiles / tiles_n) * kInvBatch : p.npix_tiles) * (p.cout_pad / bn);
+  const long inv_tiles = (p.npix_tiles / tiles_n) * ((kInvBatch + p.IMGS - 1) / p.IMGS);  // tiles of kInvBatch images
+  const long blocks = (long)(p.opt_invariant ? inv_tiles : p.npix_tiles) * (p.cout_pad / bn);
   int S = 1;
   if (x3 && bm == 256) {
     // persistent units: split K until the units cover the 256 CUs, keeping >= 4 chunks per unit

@@ -571,7 +571,18 @@ __device__ __forceinline__ void conv_x3_body(const ConvParams& p, const GnbParam
   const int nchu = (nmain + nskip) / S;  // chunks per unit (host: divisible)
   const int J = nu * nchu;
   const XDec dec = x3_dec(p, nct);
-  auto unit_of = [&](int u, int& z) { return x3_unit<SKIP>(p, dec, (int)blockIdx.x, u, z); };
+  // Four-image tiles (8 x 8 layers) at N % 4 != 0: image slot w of a tile (consumer wave w, producer wave
+  // 4 + w) past the batch recomputes the batch's last image N - 1 - by moving that wave's tile origin n0, so
+  // every read stays inside the batch and the spare slots store the very values (same image, same K order)
+  // the owning slot stores; an image's arithmetic never depends on its tile-mates (the batch-invariant mode).
+  auto unit_of = [&](int u, int& z) {
+    STile t = x3_unit<SKIP>(p, dec, (int)blockIdx.x, u, z);
+    if constexpr (Geo::IMG > 1) {
+      const int slot = wave & (Geo::IMG - 1);
+      t.n0 = min(t.n0 + slot, p.N - 1) - slot;
+    }
+    return t;
+  };
   if (IFD_TRACE && p.trace && tid == 0) {  // block entry: real time (100 MHz) and shader cycles
     p.trace[64 * blockIdx.x + 59] = __builtin_amdgcn_s_memrealtime();
     p.trace[64 * blockIdx.x + 61] = __builtin_amdgcn_s_memtime();
@@ -1315,7 +1326,7 @@ static int launch_x3_tw(const ConvParams& p, int xform, hipStream_t stream) {
 bool conv_x3_eligible(const ConvParams& p, int taps, int xform, int bn) {
   const int nch = p.cin_pad / 16 + (p.wskip ? p.cs_pad / XSK : 0);
   const bool one_img = (p.TW == 32 || p.TW == 16) && p.TH * p.TW == 256 && p.IMGS == 1;
-  const bool img8 = p.TW == 8 && p.TH == 8 && p.H == 8 && p.W == 8 && p.IMGS == 4 && p.N % 4 == 0 && !p.opt_invariant &&
+  const bool img8 = p.TW == 8 && p.TH == 8 && p.H == 8 && p.W == 8 && p.IMGS == 4 &&
                     xform == XF_NONE && (!p.res || p.res_xform == XF_NONE);
   const bool only1x1 = taps == 1 && p.cin_pad == 0 && p.wskip;  // a 1x1 conv: 1x1 chunks only
   return (taps == 9 || only1x1) && xform != XF_DOWN && bn == XBN && p.bm == 256 && (one_img || img8) &&

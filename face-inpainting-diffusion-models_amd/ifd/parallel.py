@@ -7,7 +7,9 @@ inpainted images to rank 0 (RCCL all_gather over xGMI on MI355X; gloo on CPU for
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -34,6 +36,22 @@ def device_for(local_rank):
     return torch.device("cuda", local_rank % n) if n else torch.device("cpu")
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """File descriptor 1 -> 2 for the block: the process-group setup's native libraries print connection
+    notices on stdout (gloo: "[Gloo] Rank r is connected to ..."), which must not mix into rank 0's one
+    JSON line (bench.py)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def init(backend=None, device=None):
     """Initialise the default process group when running under torch.distributed.run."""
     rank, ws, local = world()
@@ -42,10 +60,12 @@ def init(backend=None, device=None):
         if backend is None:
             shared = torch.cuda.device_count() < int(os.environ.get("LOCAL_WORLD_SIZE", ws))
             backend = "nccl" if torch.cuda.is_available() and not shared else "gloo"
-        if backend == "nccl":
-            dist.init_process_group(backend, device_id=device)
-        else:
-            dist.init_process_group(backend)
+        with _stdout_to_stderr():
+            if backend == "nccl":
+                dist.init_process_group(backend, device_id=device)
+            else:
+                dist.init_process_group(backend)
+            barrier(device)  # connections made here (lazily connecting backends print at their first collective)
     return rank, ws, local
 
 

@@ -115,3 +115,25 @@ def test_prepare_gt_mask_broadcasts_and_rejects():
     for bad_gt, bad_m in ((torch.rand(2, 3, 8, 8), m), (gt, torch.ones(4, 3, 8, 8)), (gt, torch.ones(4, 1, 4, 4))):
         with pytest.raises(ValueError):
             prepare_gt_mask(bad_gt, bad_m, 4, 8, 8, "cpu")
+
+
+def test_init_keeps_stdout_clean_gloo(tmp_path):
+    """parallel.init under torch.distributed.run (world size 2, gloo): the process group's native connection
+    notices go to stderr, so rank 0's stdout holds only what the program prints (bench.py's one JSON line;
+    gloo printed "[Gloo] Rank r is connected to ..." there before)."""
+    import subprocess
+    import sys
+    prog = tmp_path / "prog.py"
+    prog.write_text("import sys\nsys.path.insert(0, %r)\nfrom ifd import parallel\n"
+                    "r, ws, _ = parallel.init(backend='gloo')\nprint('{\"rank\": %%d}' %% r) if r == 0 else None\n"
+                    % os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                   "face-inpainting-diffusion-models_amd"))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr", "127.0.0.1", f"--master-port={port}", str(prog)],
+                         capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip() == '{"rank": 0}', out.stdout

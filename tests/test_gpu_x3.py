@@ -145,6 +145,34 @@ def test_x3_matches_fp32_batch4(x3_model):
     assert maxabs(y1, y3[2:3]) <= 2e-5
 
 
+def test_x3_invariant_partial_image_tiles():
+    """Batch-invariant geometry at B = 5: the 8x8 layers run as four-image tiles at any batch (the last tile
+    holds one image; its spare slots recompute that image, conv_x3.hip unit_of). Against the fp32 mode, and
+    images 0 and 4 (a full and a partial tile) bit for bit against their own B = 1 runs, which are partial
+    tiles of one image."""
+    from ifd.model import DiffusionInpaintingModel
+    g = torch.Generator(device=DEV).manual_seed(13)
+    x = torch.randn(5, 3, 256, 256, device=DEV, generator=g)
+    gt = torch.rand(5, 3, 256, 256, device=DEV, generator=g) * 2 - 1
+    mask = (torch.rand(5, 1, 256, 256, device=DEV, generator=g) > 0.5).float()
+    t = torch.tensor([999, 640, 120, 7, 450], device=DEV)
+    mi = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16", options={"batch_invariant": 1})
+    mi.load_state_dict(make_state_dict(FULL, seed=1))
+    m32 = DiffusionInpaintingModel(FULL, device=DEV, precision="fp32")
+    m32.load_state_dict(make_state_dict(FULL, seed=1))
+    mk = gt * (1 - mask)
+    with torch.no_grad():
+        y, ks = _kernels_run(mi, lambda: mi(x, t, masked_image=mk, mask=mask))
+        y32 = m32(x, t, masked_image=mk, mask=mask)
+        ys = [mi(x[i:i + 1], t[i:i + 1], masked_image=mk[i:i + 1], mask=mask[i:i + 1]) for i in (0, 4)]
+    assert any(k.startswith("conv_x3_kernel") and k.endswith(",8,3>") for k in ks), sorted(ks)
+    assert torch.isfinite(y).all()
+    err = maxabs(y, y32)
+    print(f"3xf16 invariant vs fp32 B=5 maxabs={err:.3g}")
+    assert err <= 2e-5
+    assert torch.equal(ys[0], y[0:1]) and torch.equal(ys[1], y[4:5])
+
+
 def test_x3_matches_fp32_bench_batch(x3_model):
     """The bench configuration itself (B=16 at 256x256, the geometry bench.py times: blk_major
     units, four-image 8x8 tiles, split-K 1x1 launches): 3xf16 against fp32 at two timesteps."""
