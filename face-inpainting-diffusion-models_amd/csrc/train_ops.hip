@@ -1270,6 +1270,9 @@ struct GnBwdArgs {
   // arithmetic), and radd (optional, same resolution: the skip path's gradient) joins dx through it as well
   int rmode = 0, W = 0;
   const float* radd = nullptr;
+  // optional split output (concat inputs): dx gets channels [0, C0) as [N][HW][C0] and dx1 channels [C0, C) as
+  // [N][HW][C - C0] - the gradient of each concat source in its own tensor (no channel copy out of a C-wide one)
+  float* dx1 = nullptr;
 };
 // the resample adjoint of t (at the output resolution) at GroupNorm-input pixel p of image n, channels c0..c0+3
 __device__ __forceinline__ f32x4 gn_radj(const GnBwdArgs& a, const float* t, int n, int p, int c0) {
@@ -1482,7 +1485,7 @@ __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(GnBwdArgs a, const float
     const f32x4 xv = *reinterpret_cast<const f32x4*>(xb + (int64_t)p * xs);
     const f32x4 dv = a.rmode ? gn_radj(a, a.dout, n, p, c0) : *reinterpret_cast<const f32x4*>(a.dout + i);
     f32x4 prev = {0.f, 0.f, 0.f, 0.f};
-    if (accumulate) prev = *reinterpret_cast<const f32x4*>(dx + i);
+    if (accumulate) prev = *reinterpret_cast<const f32x4*>(dx + i);  // (never with a split output: host-checked)
     if (a.add) prev += *reinterpret_cast<const f32x4*>(a.add + ((int64_t)n * a.HW + p) * a.add_stride + c0);
     if (a.radd) prev += gn_radj(a, a.radd, n, p, c0);
     f32x4 o;
@@ -1500,7 +1503,12 @@ __global__ __launch_bounds__(256) void gn_bwd_dx_kernel(GnBwdArgs a, const float
       const float v = rstd[j] * (dxhat - r0[j] - xhat * r1[j]);
       o[j] = accumulate || a.add || a.radd ? prev[j] + v : v;
     }
-    *reinterpret_cast<f32x4*>(dx + i) = o;
+    float* dst = dx + i;
+    if (a.dx1) {  // (uniform per thread: its channel quad sits in one source)
+      const int64_t px = (int64_t)n * a.HW + p;
+      dst = c0 < a.C0 ? dx + px * a.C0 + c0 : a.dx1 + px * (C - a.C0) + (c0 - a.C0);
+    }
+    *reinterpret_cast<f32x4*>(dst) = o;
   }
 }
 
@@ -2924,13 +2932,14 @@ int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const
                   const float* ss, int ss_stride, int act_silu, const float* stats, float* dx, int accumulate,
                   float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, void* stream) {
   return ifd_tr_gn_bwd_cat(dout, x, C, nullptr, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, dx, accumulate,
-                           dgamma, dbeta, dss, work, work_floats, nullptr, 0, stream);
+                           dgamma, dbeta, dss, work, work_floats, nullptr, 0, nullptr, stream);
 }
 
 int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
                       const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                       const float* stats, float* dx, int accumulate, float* dgamma, float* dbeta, float* dss,
-                      float* work, int64_t work_floats, const float* add, int add_stride, void* stream) {
+                      float* work, int64_t work_floats, const float* add, int add_stride, float* dx1,
+                      void* stream) {
   const int nsl = gn_nsl(HW, N, C);
   const int64_t need = (int64_t)N * nsl * C * 3 + (int64_t)N * C * 3 + (int64_t)N * 64;
   if (C % 32 || C > 1024 || need > work_floats || C0 % 4 || C0 <= 0 || C0 > C || (C0 < C && !x1)) {
@@ -2941,9 +2950,14 @@ int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x
     set_error("ifd_tr_gn_bwd: addend stride must be >= C, in quads, 16-B aligned");
     return 2;
   }
+  if (dx1 && (C0 == C || accumulate || ((uintptr_t)dx1 & 15))) {
+    set_error("ifd_tr_gn_bwd: a split output needs a concat input (C0 < C), accumulate 0, 16-B aligned");
+    return 2;
+  }
   GnBwdArgs a{dout, x0, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, x1, C0};
   a.add = add;
   a.add_stride = add_stride;
+  a.dx1 = dx1;
   float* part = work;
   float* nc = work + (int64_t)N * nsl * C * 3;
   float* red = nc + (int64_t)N * C * 3;
@@ -2991,7 +3005,7 @@ int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const fl
                             const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                             const float* stats, const float* part, int part_nsl, float* dx, int accumulate,
                             float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, const float* add,
-                            int add_stride, void* stream) {
+                            int add_stride, float* dx1, void* stream) {
   const int64_t need = (int64_t)N * C * 3 + (int64_t)N * 64;
   const int nsl = gn_nsl(HW, N, C);  // the dx pass keeps its own pixel slices
   if (C % 32 || C > 1024 || need > work_floats || C0 % 4 || C0 <= 0 || C0 > C || (C0 < C && !x1) || !part ||
@@ -3003,9 +3017,14 @@ int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const fl
     set_error("ifd_tr_gn_bwd: addend stride must be >= C, in quads, 16-B aligned");
     return 2;
   }
+  if (dx1 && (C0 == C || accumulate || ((uintptr_t)dx1 & 15))) {
+    set_error("ifd_tr_gn_bwd: a split output needs a concat input (C0 < C), accumulate 0, 16-B aligned");
+    return 2;
+  }
   GnBwdArgs a{dout, x0, N, HW, C, gamma, beta, ss, ss_stride, act_silu, stats, x1, C0};
   a.add = add;
   a.add_stride = add_stride;
+  a.dx1 = dx1;
   float* nc = work;
   float* red = nc + (int64_t)N * C * 3;
   hipStream_t s = (hipStream_t)stream;

@@ -51,13 +51,13 @@ TRAIN_EXPORTS = {
     "ifd_tr_conv_wgrad_x3_gn": (i32, [vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp, i64, vp, i32,
                                       vp]),
     "ifd_tr_gn_bwd_cat": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, vp, i64,
-                                vp, i32, vp]),
+                                vp, i32, vp, vp]),
     "ifd_tr_gn_slices": (i64, [i32, i32, i32]),
     "ifd_tr_gnb_part_floats": (i64, [i32, i32, i32]),
     "ifd_tr_conv_x3_gnb": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp, vp, vp, vp, i32,
                                  i32, vp, i64, _c.POINTER(i32), i32, vp]),
     "ifd_tr_gn_bwd_from_part": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, i32, vp, vp,
-                                      vp, vp, i64, vp, i32, vp]),
+                                      vp, vp, i64, vp, i32, vp, vp]),
     "ifd_tr_gn_coef": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, i32, f32, vp, vp, vp, vp, i64, vp]),
     "ifd_tr_act_apply": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp]),
     "ifd_tr_act_resample": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, vp]),
@@ -527,36 +527,48 @@ class UNetTrainer:
         return _c.c_void_p(t.data_ptr() + 4 * off), stride
 
     def gn_bwd(self, dout, x, N, HW, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None, silu=True, x1=None,
-               C0=None, add=None):
+               C0=None, add=None, split=None):
         """x1, C0: the GroupNorm input is concat(x[C0], x1[C - C0]) (read by channel range). add = (t, stride,
-        offset): dx also gets that channel range of t (ifd_tr_gn_bwd_cat)."""
-        acc = dx is not None
-        if dx is None:
-            dx = self._empty(N * HW * C)
-        else:
-            self._dirty(dx)
+        offset): dx also gets that channel range of t (ifd_tr_gn_bwd_cat). split = (d0, d1): the gradient is
+        written per concat source, d0 [.., C0] and d1 [.., C - C0] (returned as that pair; dx must be None)."""
+        dx, dx1, acc = self._gn_bwd_out(dx, split, N * HW * C)
         nsl = lib().ifd_tr_gn_slices(HW, N, C)
         work = self._empty(N * nsl * C * 3 + N * C * 3 + N * 64)
         chk(lib().ifd_tr_gn_bwd_cat(P(dout), P(x), C0 if x1 is not None else C, P(x1), N, HW, C,
                                     P(self.p(prefix + "weight")), P(self.p(prefix + "bias")), P(ss), ss_stride,
                                     int(silu), P(stats), P(dx), int(acc), P(self.g(prefix + "weight")),
                                     P(self.g(prefix + "bias")), P(dss), P(work), work.numel(), *self._addend(add),
-                                    self.s))
-        return dx
+                                    P(dx1), self.s))
+        return (dx, dx1) if split is not None else dx
+
+    def _gn_bwd_out(self, dx, split, numel):
+        """The GroupNorm backward's output: (dx, dx1, accumulate) for dx = given (+=), a split pair, or fresh."""
+        if split is not None:
+            if dx is not None:
+                raise ValueError("gn_bwd: a split output does not accumulate")
+            for t in split:
+                self._dirty(t)
+            return split[0], split[1], False
+        if dx is None:
+            return self._empty(numel), None, False
+        self._dirty(dx)
+        return dx, None, True
 
     def dgrad_gn_bwd(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None,
-                     silu=True, x1=None, C0=None, add=None):
+                     silu=True, x1=None, C0=None, add=None, split=None):
         """gn_bwd(conv^T(dy)) - the dgrad of conv `wname` fed into the GroupNorm backward of its input x (C
         channels; x1 / C0 as gn_bwd). On the split kernel the GroupNorm's pass 1 runs in the dgrad's epilogue
         (ifd_tr_conv_x3_gnb); shapes it does not take run conv() then gn_bwd()."""
-        out = self._dgrad_gnb(dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0, add)
+        out = self._dgrad_gnb(dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0, add,
+                              split)
         if out is not None:
             return out
         da = self.conv(dy, cdy, N, H, wname, transpose=True)
         return self.gn_bwd(da, x, N, H * H, C, prefix, stats, dx=dx, ss=ss, ss_stride=ss_stride, dss=dss, silu=silu,
-                           x1=x1, C0=C0, add=add)
+                           x1=x1, C0=C0, add=add, split=split)
 
-    def _dgrad_gnb(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0, add=None):
+    def _dgrad_gnb(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0, add=None,
+                   split=None):
         if not (self.fuse_gnb and self._x3_active(True)):
             return None
         w = self.p(wname)
@@ -586,18 +598,14 @@ class UNetTrainer:
         chk(rc)
         if nsl.value == 0:  # (the conv ran; its geometry could not carry the partial sums)
             return self.gn_bwd(da, x, N, H * H, C, prefix, stats, dx=dx, ss=ss, ss_stride=ss_stride, dss=dss,
-                               silu=silu, x1=x1, C0=C0, add=add)
-        acc = dx is not None
-        if dx is None:
-            dx = self._empty(N * H * H * C)
-        else:
-            self._dirty(dx)
+                               silu=silu, x1=x1, C0=C0, add=add, split=split)
+        dx, dx1, acc = self._gn_bwd_out(dx, split, N * H * H * C)
         work = self._empty(N * C * 3 + N * 64)
         chk(lib().ifd_tr_gn_bwd_from_part(P(da), P(x), c0, P(x1), N, H * H, C, P(gam), P(bet), P(ss), ss_stride,
                                           int(silu), P(stats), P(gpart), nsl.value, P(dx), int(acc),
                                           P(self.g(prefix + "weight")), P(self.g(prefix + "bias")), P(dss), P(work),
-                                          work.numel(), *self._addend(add), self.s))
-        return dx
+                                          work.numel(), *self._addend(add), P(dx1), self.s))
+        return (dx, dx1) if split is not None else dx
 
     def resample(self, x, N, Hin, C, mode):
         Ho = 2 * Hin if mode == 1 else Hin // 2
@@ -819,7 +827,9 @@ class UNetTrainer:
                 # the middle block's input is the last input block's output: its first layer's dx also takes that
                 # block's skip gradient (filled by the output blocks above)
                 last = section == "middle" and i == len(layers) - 1
-                dh, r = self._layer_bwd(L, dh, N, saved, demb, add=self._skip_addend(dhs[-1]) if last else None)
+                first_out = section == "output" and i == len(layers) - 1
+                dh, r = self._layer_bwd(L, dh, N, saved, demb, add=self._skip_addend(dhs[-1]) if last else None,
+                                        split=first_out)
                 if last:
                     dhs[-1] = None
             if section == "output":
@@ -827,12 +837,16 @@ class UNetTrainer:
                 cin = layers[0]["cin"]
                 sc = layers[0]["skip_ch"]
                 hcur = cin - sc
-                dprev = self._empty(N, r, r, hcur)
-                self.copy_ch(dh, cin, 0, dprev, hcur, 0, hcur, N * r * r, False)
-                # the skip part stays in d cat until the input chain accumulates it (no copy of its own)
-                dhs[hs_idx] = (dh, cin, hcur, sc, N * r * r)
+                if isinstance(dh, tuple):  # already per source (the concat was never materialised)
+                    dh, dskip = dh
+                    dhs[hs_idx] = (dskip, sc, 0, sc, N * r * r)
+                else:
+                    dprev = self._empty(N, r, r, hcur)
+                    self.copy_ch(dh, cin, 0, dprev, hcur, 0, hcur, N * r * r, False)
+                    # the skip part stays in d cat until the input chain accumulates it (no copy of its own)
+                    dhs[hs_idx] = (dh, cin, hcur, sc, N * r * r)
+                    dh = dprev
                 hs_idx += 1
-                dh = dprev
         # middle block's input = the last input block's output: dh continues down the input chain. Input block
         # b's output gradient = the chain's + its skip part in d cat (dhs[b]): added where block b + 1's first
         # layer writes its dx (the GroupNorm backward's addend), else by a channel copy
@@ -865,8 +879,10 @@ class UNetTrainer:
         dcat, cin, off, sc, npix = rec
         return (dcat, cin, off)
 
-    def _layer_bwd(self, L, dout, N, saved, demb, add=None):
-        """add: (t, stride, offset) added into the layer's input gradient (a ResBlock's GroupNorm dx pass)."""
+    def _layer_bwd(self, L, dout, N, saved, demb, add=None, split=False):
+        """add: (t, stride, offset) added into the layer's input gradient (a ResBlock's GroupNorm dx pass).
+        split: an output block's first ResBlock over concat(h, skip) (never materialised) returns its input
+        gradient per source, (d h, d skip), instead of one C-wide tensor."""
         k, p = L["kind"], L["prefix"]
         if k == "attn":
             if add is not None:
@@ -929,8 +945,16 @@ class UNetTrainer:
             # the skip path's gradient (dout itself, or the 1x1 conv's fresh dgrad) is the accumulation
             # target of the GroupNorm input gradient: no separate add pass; the dgrad of in_layers.2 carries
             # the GroupNorm backward's pass 1 (dgrad_gn_bwd)
-            dx = self.dgrad_gn_bwd(dh1, cout, N, ro, p + "in_layers.2.weight", sv["x"], cin, p + "in_layers.0.",
-                                   sv["st1"], dx=dxr, silu=True, x1=x1, C0=c0, add=add)
+            if split and x1 is not None:
+                # the skip path's gradient joins as the addend and dx comes out per concat source
+                if add is not None:
+                    raise ValueError("a split input gradient takes no other addend")
+                pair = (self._empty(N, r, r, c0), self._empty(N, r, r, c1))
+                dx = self.dgrad_gn_bwd(dh1, cout, N, ro, p + "in_layers.2.weight", sv["x"], cin, p + "in_layers.0.",
+                                       sv["st1"], silu=True, x1=x1, C0=c0, add=(dxr, cin, 0), split=pair)
+            else:
+                dx = self.dgrad_gn_bwd(dh1, cout, N, ro, p + "in_layers.2.weight", sv["x"], cin, p + "in_layers.0.",
+                                       sv["st1"], dx=dxr, silu=True, x1=x1, C0=c0, add=add)
         return dx, r
 
     # ------------------------------------------------------------------ loss / step

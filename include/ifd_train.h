@@ -151,11 +151,14 @@ int ifd_tr_gn_bwd(const float* dout, const float* x, int N, int HW, int C, const
 /* ifd_tr_gn_bwd of a concat input x = concat(x0[C0], x1[C - C0]) read by channel range (the output blocks'
  * cat(h, skip), code/unet.py:170); dx is the concat's gradient as one [N][HW][C] tensor. add (optional, else
  * NULL): dx also gets add[p * add_stride + c] (a channel range of a wider tensor: the skip part of an output
- * block's concat gradient, which joins the encoder chain's gradient here instead of by a separate pass). */
+ * block's concat gradient, which joins the encoder chain's gradient here instead of by a separate pass).
+ * dx1 (optional, else NULL; C0 < C, accumulate 0): the gradient split per concat source - dx [N][HW][C0] gets
+ * channels [0, C0), dx1 [N][HW][C - C0] channels [C0, C) (no channel copy out of a C-wide gradient). */
 int ifd_tr_gn_bwd_cat(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
                       const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                       const float* stats, float* dx, int accumulate, float* dgamma, float* dbeta, float* dss,
-                      float* work, int64_t work_floats, const float* add, int add_stride, void* stream);
+                      float* work, int64_t work_floats, const float* add, int add_stride, float* dx1,
+                      void* stream);
 /* ifd_tr_gn_bwd (no scale/shift, one source) for a resampling ResBlock's in_layers GroupNorm (code/nn.py:
  * 189-195): dout at the block's output resolution (mode 1: nearest-up x2, 2H; mode 2: AvgPool2d(2), H/2) is read
  * through the resample adjoint, and radd (optional, same resolution: the skip path's gradient) joins dx through
@@ -176,13 +179,13 @@ int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, 
                        const float* gx1, const float* stats, const float* gamma, const float* beta, const float* ss,
                        int ss_stride, int act_silu, float* gpart, int64_t gpart_floats, int* gpart_nsl, int nprod,
                        void* stream);
-/* ifd_tr_gn_bwd_cat with pass 1 done (gpart from ifd_tr_conv_x3_gnb): reduce, group, parameter and dx passes.
- * work: N*C*3 + N*64 floats. */
+/* ifd_tr_gn_bwd_cat with pass 1 done (gpart from ifd_tr_conv_x3_gnb): reduce, group, parameter and dx passes
+ * (add, dx1 as there). work: N*C*3 + N*64 floats. */
 int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,
                             const float* gamma, const float* beta, const float* ss, int ss_stride, int act_silu,
                             const float* stats, const float* part, int part_nsl, float* dx, int accumulate,
                             float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, const float* add,
-                            int add_stride, void* stream);
+                            int add_stride, float* dx1, void* stream);
 /* nearest-up x2 (mode 1) / AvgPool2d(2) (mode 2) (code/nn.py:92-133) and the adjoint (dx at Hin). */
 int ifd_tr_resample(const float* x, int N, int Hin, int C, int mode, float* out, void* stream);
 int ifd_tr_resample_bwd(const float* dy, int N, int Hin, int C, int mode, float* dx, int accumulate, void* stream);

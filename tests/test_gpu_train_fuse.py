@@ -229,12 +229,12 @@ def test_conv_x3_gnb_partials_match_separate_pass(record):
                 wk = torch.empty(N * C * 3 + N * 64, device=DEV)
                 chk(lib().ifd_tr_gn_bwd_from_part(P(da), P(x0), C0, P(x1), N, H * H, C, P(gam), P(bet), P(ss),
                                                   2 * C if use_ss else 0, 1, P(st), P(gpart), nsl.value, P(dx), 0, P(dg),
-                                                  P(db), P(dss), P(wk), wk.numel(), None, 0, s))
+                                                  P(db), P(dss), P(wk), wk.numel(), None, 0, None, s))
             else:
                 wk = torch.empty(N * nsl0 * C * 3 + N * C * 3 + N * 64, device=DEV)
                 chk(lib().ifd_tr_gn_bwd_cat(P(da), P(x0), C0, P(x1), N, H * H, C, P(gam), P(bet), P(ss),
                                             2 * C if use_ss else 0, 1, P(st), P(dx), 0, P(dg), P(db), P(dss), P(wk),
-                                            wk.numel(), None, 0, s))
+                                            wk.numel(), None, 0, None, s))
             torch.cuda.synchronize()
             outs[fused] = (dx, dg, db, dss)
         assert int(guard.max()) == 0
@@ -327,7 +327,7 @@ def test_concat_sources_match_materialised(N, H, c0, c1, cout, record):
         work = torch.empty(N * nsl * C * 3 + N * C * 3 + N * 64, device=DEV)
         x0, cc0, x1 = (xa, c0, xb) if two else (cat, C, None)
         chk(lib().ifd_tr_gn_bwd_cat(P(da), P(x0), cc0, P(x1), N, H * H, C, P(gamma), P(beta), None, 0, 1, P(st), P(dx),
-                                    0, P(dgam), P(dbet), None, P(work), work.numel(), None, 0, s))
+                                    0, P(dgam), P(dbet), None, P(work), work.numel(), None, 0, None, s))
         gx.append((dx, dgam, dbet))
     torch.cuda.synchronize()
     assert int(guard.max()) == 0
@@ -365,10 +365,53 @@ def test_gn_bwd_addend(N, H, C, stride, off):
         work = torch.empty(N * nsl * C * 3 + N * C * 3 + N * 64, device=DEV)
         ap = ctypes.c_void_p(wide.data_ptr() + 4 * off) if add else None
         chk(lib().ifd_tr_gn_bwd_cat(P(dout), P(x), C, None, N, H * H, C, P(gam), P(bet), None, 0, 1, P(st), P(dx), 0,
-                                    P(dg), P(db), None, P(work), work.numel(), ap, stride if add else 0, s))
+                                    P(dg), P(db), None, P(work), work.numel(), ap, stride if add else 0, None, s))
         outs.append((dx, dg, db))
     torch.cuda.synchronize()
     ref = outs[0][0] + wide[..., off:off + C]
     err = (outs[1][0] - ref).abs()
     assert float(err.max()) <= 2.0 ** -22 * float(ref.abs().max()), float(err.max())
     assert torch.equal(outs[1][1], outs[0][1]) and torch.equal(outs[1][2], outs[0][2])
+
+
+@pytest.mark.parametrize("N,H,C0,C1", [(2, 16, 128, 128), (3, 8, 192, 64)])
+def test_gn_bwd_split_output(N, H, C0, C1):
+    """ifd_tr_gn_bwd_cat's split output (the output blocks' concat gradient per source, no channel copy out of the
+    C-wide gradient): with the skip conv's gradient as the addend, dx [.., C0] and dx1 [.., C1] equal the two channel
+    ranges of the C-wide dx bit for bit (same arithmetic, other addresses), and the parameter gradients are equal."""
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    C = C0 + C1
+    g = torch.Generator().manual_seed(9)
+    xa = torch.randn(N, H * H, C0, generator=g).to(DEV)
+    xb = torch.randn(N, H * H, C1, generator=g).to(DEV)
+    dout = torch.randn(N, H * H, C, generator=g).to(DEV)
+    wide = torch.randn(N, H * H, C, generator=g).to(DEV)
+    gam = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    st = torch.empty(N * 64, device=DEV)
+    nsl = lib().ifd_tr_gn_slices(H * H, N, C)
+    wk = torch.empty(N * nsl * 64, device=DEV, dtype=torch.float64)
+    cat = torch.cat([xa, xb], -1).contiguous()
+    chk(lib().ifd_tr_gn_fwd(P(cat), N, H * H, C, P(gam), P(bet), None, 0, 1, P(torch.empty_like(cat)), P(st), P(wk),
+                            wk.numel(), s))
+    outs = []
+    for split in (False, True):
+        dx = torch.empty(N, H * H, C0 if split else C, device=DEV)
+        dx1 = torch.empty(N, H * H, C1, device=DEV) if split else None
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        work = torch.empty(N * nsl * C * 3 + N * C * 3 + N * 64, device=DEV)
+        chk(lib().ifd_tr_gn_bwd_cat(P(dout), P(xa), C0, P(xb), N, H * H, C, P(gam), P(bet), None, 0, 1, P(st), P(dx),
+                                    0, P(dg), P(db), None, P(work), work.numel(), P(wide), C, P(dx1), s))
+        outs.append((dx, dx1, dg, db))
+    torch.cuda.synchronize()
+    (w, _, dg0, db0), (d0, d1, dg1, db1) = outs
+    assert torch.equal(d0, w[..., :C0]) and torch.equal(d1, w[..., C0:])
+    assert torch.equal(dg0, dg1) and torch.equal(db0, db1)
+    # a split output is refused with accumulate or a single-source input
+    from ifd import _lib as L
+    with pytest.raises(RuntimeError):
+        L.check(lib().ifd_tr_gn_bwd_cat(P(dout), P(xa), C0, P(xb), N, H * H, C, P(gam), P(bet), None, 0, 1, P(st),
+                                        P(d0), 1, P(dg), P(db), None, P(work), work.numel(), None, 0, P(d1), s))
