@@ -1,6 +1,6 @@
 """Development probe: one fused DDIM step (ifd_ddim_step, B = 16 at 256^2) launched eagerly vs replayed from a
 HIP graph captured once (same arguments), to price the GPU-side launch gaps of the ~188 kernels per UNet eval.
-usage: python tools/graph_probe.py [steps]"""
+usage: python tools/graph_probe.py [steps] [batch]"""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "face-inpainting-diffusion-models_amd"))
 import numpy as np
@@ -13,7 +13,7 @@ from ifd.schedules import create_gaussian_diffusion
 from ifd.topology import FULL
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-B = 16
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 dev = torch.device("cuda:0")
 m = DiffusionInpaintingModel(FULL, device=dev)
 m.load_state_dict(make_state_dict(FULL, seed=1))
