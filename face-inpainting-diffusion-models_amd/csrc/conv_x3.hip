@@ -255,7 +255,9 @@ struct XProducer {
       const bool inb = ldso[i] >= 0 && y >= 0 && y < p.H && x >= 0 && x < p.W;
       int sy = y, sx = x;
       if (XF == XF_UP) { sy = y >> 1; sx = x >> 1; }
-      const int sp = inb ? (hi[i] * p.Hin + sy) * p.Win + sx : 0;
+      // a padding pixel reads its own image's first pixel (times valid = 0): the base is the tile origin n0, which
+      // a partial four-image tile moves below 0 for its spare slots (unit_of), so offset 0 is not in the batch
+      const int sp = inb ? (hi[i] * p.Hin + sy) * p.Win + sx : hi[i] * p.Hin * p.Win;
       valid[i] = inb ? 1.f : 0.f;
       off0[i] = (sp * p.c0 + 8 * hh) * 4;
       off1[i] = (sp * p.c1 + 8 * hh) * 4;
