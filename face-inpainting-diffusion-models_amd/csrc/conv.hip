@@ -563,9 +563,9 @@ void conv_geometry(ConvParams& p, int H, int W, int N, int bn, int nchunks, bool
     // 3xf16 split kernel (conv_x3.hip): 256-pixel tiles of one image (8 x 32 or 16 x 16) whatever
     // the tile count (persistent grid); nchunks = 16-channel chunks of the whole K stream
     if (bn == 64 && W >= 16 && H >= 256 / (W < 32 ? W : 32)) bm = 256;
-    // four whole 8 x 8 images per tile, at any N (a partial last tile recomputes the batch's last image in its
-    // spare slots, conv_x3.hip unit_of)
-    if (bn == 64 && W == 8 && H == 8) bm = 256;
+    // four whole 8 x 8 images per tile; with opt_img8_partial at any N (a partial last tile recomputes the
+    // batch's last image in its spare slots, conv_x3.hip unit_of)
+    if (bn == 64 && W == 8 && H == 8 && (N % 4 == 0 || p.opt_img8_partial)) bm = 256;
   } else if (allow256 && bn == 64 && W >= 32 && H >= 8) {
     const long blocks256 = (long)(p.opt_invariant ? kInvBatch : N) * (H / 8) * (W / 32) * (p.cout_pad / bn);
     if (blocks256 >= 512) bm = 256;

@@ -681,6 +681,186 @@ __global__ __launch_bounds__(WxCfg<1>::NT, 1) void wgrad_x3_kernel(WgArgs a, uns
   }
 }
 
+// Wide-tile 1x1 weight gradient (the output blocks' skip connections at 128^2 / 256^2: cout = 128 over a 256- or
+// 384-channel concat): dW[co][ci] = sum_p dY[p][co] X[p][ci] for a 128 co x 128 ci tile per block, so a layer's
+// X is read once and dY once per 128 input channels (wgrad_x3_kernel's 64 x 64 tiles read X cout / 64 and dY
+// cin / 64 times, and staged 0.67 KB per MFMA: 1.8 ms for the 256^2 256 -> 128 layer at B = 32, 1.8 TB/s of
+// algorithmic bytes). Same arithmetic per product as wgrad_x3_kernel (split hi / lo, NPROD f16 products into one
+// fp32 accumulator per output, k-steps of 16 pixels in pixel order, splits summed by slab_bias_reduce_kernel).
+// 4 waves, one 64 co x 64 ci quadrant each (2 x 2 MFMA tiles, one 64-channel LDS plane of each operand);
+// chunks of 32 consecutive pixels (NHWC rows, never across images: HW % 32 == 0), staged pixel-major at
+// wgrad_x3_kernel's 96-f16 pitch and read through ds_read_b64_tr_b16. Chunk c + 1 is staged between chunk
+// c's k-steps, loads go out two chunks ahead (two register sets, as wgrad_x3_kernel).
+constexpr int WW_PX = 32;                    // pixels per chunk (2 k-steps)
+constexpr int WW_PL = WW_PX * WX_P;          // one 64-channel plane of one part: 32 rows at the 96-f16 pitch
+constexpr int WW_OP = 2 * 2 * WW_PL;         // one operand: [part hi / lo][plane 0 / 1]
+constexpr int WW_ST = 2 * WW_OP;             // one stage: dY then X
+constexpr int WW_NT = 256;
+static_assert(2 * WW_ST * 2 <= 160 * 1024, "two stages fit the LDS");
+// eligible shapes (the host also needs 128-channel tiles inside one concat source)
+__host__ __device__ constexpr bool ww_shape(int cout, int cin) { return cout == 128 && cin % 128 == 0 && cin <= 512; }
+
+template <int NPROD>
+__global__ __launch_bounds__(WW_NT, 1) void wgrad1x1_wide_kernel(WgArgs a, unsigned* guard, float* colpart) {
+  __shared__ __attribute__((aligned(16))) _Float16 lds[2][WW_ST];
+  f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop (its last barrier)
+  const int cin = a.c0 + a.c1;
+  const int cit = blockIdx.x, zs = blockIdx.y;
+  const int ci0 = cit * 128;
+  const bool src1 = a.c1 && ci0 >= a.c0;  // the tile's X source (block-uniform; host: 128-channel tiles in one)
+  const float* const xsrc = src1 ? a.x1 : a.x0;
+  const int xst = src1 ? a.c1 : a.c0, xc0 = src1 ? ci0 - a.c0 : ci0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5;
+  const int HW = a.H * a.W;
+  const int64_t nch = a.P / WW_PX;
+  const int64_t c_beg = (int64_t)zs * a.chunks_per_split;
+  const int64_t c_end = c_beg + a.chunks_per_split < nch ? c_beg + a.chunks_per_split : nch;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float gmax = 0.f;
+  const bool do_cs = colpart && cit == 0;
+  f32x4 csum = {0.f, 0.f, 0.f, 0.f};
+  // staging items: channel quad cq = tid & 31 (the same for every item of the thread: one co quad of dY, one ci
+  // quad of X), pixel rows pr + 8 k, k < 4, of each operand
+  const int cq = tid & 31, pr = tid >> 5;
+  const int pl = cq >> 4, col = 4 * (cq & 15);  // LDS plane (64 channels) and column of the quad
+  if (c_beg < c_end) {
+    f32x4 dvs[2][4], xvs[2][4];
+    auto load = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
+      f32x4(&dv)[4] = dvs[decltype(SETc)::value];
+      f32x4(&xv)[4] = xvs[decltype(SETc)::value];
+      const int64_t p0 = c * WW_PX;
+      const int n = (int)(p0 / HW), q0 = (int)(p0 - (int64_t)n * HW);  // image, its first pixel (chunks stay in it)
+      const rsrc_t rd = mkrsrc(a.dy + (size_t)n * HW * a.cout);
+      const rsrc_t rx = mkrsrc(xsrc + (size_t)n * HW * xst);
+      const int od = __builtin_amdgcn_readfirstlane(q0 * a.cout * 4), ox = __builtin_amdgcn_readfirstlane(q0 * xst * 4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        dv[k] = bld4(rd, ((pr + 8 * k) * a.cout + 4 * cq) * 4 + od, 0);
+        xv[k] = bld4(rx, ((pr + 8 * k) * xst + xc0 + 4 * cq) * 4 + ox, 0);
+      }
+    };
+    auto store_item = [&](_Float16* L, int it, auto SETc) __attribute__((always_inline)) {
+      const f32x4(&dv)[4] = dvs[decltype(SETc)::value];
+      const f32x4(&xv)[4] = xvs[decltype(SETc)::value];
+      const bool isd = it < 4;
+      const int k = it & 3;
+      const f32x4 v = isd ? dv[k] : xv[k];
+      if (isd && do_cs) csum += v;
+      unsigned h0, l0, h1, l1;
+      wx_split2(v[0], v[1], h0, l0);
+      wx_split2(v[2], v[3], h1, l1);
+      asm("v_max3_f32 %0, %0, |%1|, |%2|\n\tv_max3_f32 %0, %0, |%3|, |%4|"
+          : "+v"(gmax)
+          : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+      _Float16* O = L + (isd ? 0 : WW_OP) + pl * WW_PL + wx_off(pr + 8 * k, col);
+      *(wx_lds_u2*)O = wx_u2{h0, h1};
+      if (NPROD == 3) *(wx_lds_u2*)(O + 2 * WW_PL) = wx_u2{l0, l1};
+    };
+    // fragment roles (wgrad_x3_kernel's transposed reads): group G = lane >> 4, lane 4q + p of the group
+    // addresses row q, columns 4p .. 4p + 3; the wave's quadrant is plane (wave & 1) of dY, (wave >> 1) of X
+    const int G = lane >> 4, q = (lane & 15) >> 2, pcol = 4 * (lane & 3);
+    const int cf = 16 * (G & 1) + pcol;
+    auto mfma_chunk = [&](const _Float16* L, _Float16* Ln, bool nxt, auto SETc) __attribute__((always_inline)) {
+      int cfl = cf, ql = q, hl = h;
+      asm volatile("" : "+v"(cfl), "+v"(ql), "+v"(hl));
+      const _Float16* pA = L + (wave & 1) * WW_PL + (8 * hl + ql) * WX_P + cfl;
+      const _Float16* pB = L + WW_OP + (wave >> 1) * WW_PL + (8 * hl + ql) * WX_P + cfl;
+      auto frag = [&](const _Float16* p0, int st, int t, wx_h8& hi, wx_h8& lo) {
+        const _Float16* b = p0 + 16 * st * WX_P + 32 * t;
+        const wx_h4 h0v = wx_tr(b, 0), h1v = wx_tr(b, 4 * WX_P);
+        hi = wx_h8{h0v[0], h0v[1], h0v[2], h0v[3], h1v[0], h1v[1], h1v[2], h1v[3]};
+        if (NPROD == 3) {
+          const wx_h4 l0v = wx_tr(b, 2 * WW_PL), l1v = wx_tr(b, 2 * WW_PL + 4 * WX_P);
+          lo = wx_h8{l0v[0], l0v[1], l0v[2], l0v[3], l1v[0], l1v[1], l1v[2], l1v[3]};
+        } else {
+          lo = hi;
+        }
+      };
+#pragma unroll
+      for (int st = 0; st < WW_PX / 16; ++st) {
+        wx_h8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          frag(pA, st, t, ah[t], al[t]);
+          frag(pB, st, t, bh[t], bl[t]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = WX_MFMA(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (nxt)  // (block-uniform) chunk c + 1's staging, half of it per k-step
+#pragma unroll
+          for (int it = 4 * st; it < 4 * st + 4; ++it) store_item(Ln, it, SETc);
+        __builtin_amdgcn_sched_barrier(0);
+        if (NPROD == 3) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = WX_MFMA(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = WX_MFMA(al[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    const std::integral_constant<int, 0> set0;
+    const std::integral_constant<int, 1> set1;
+    load(c_beg, set0);
+#pragma unroll
+    for (int it = 0; it < 8; ++it) store_item(lds[c_beg & 1], it, set0);
+    __syncthreads();
+    // (loads past the block's range re-read its last chunk: every iteration issues the same loads)
+    auto clampc = [&](int64_t c) { return c < c_end ? c : c_end - 1; };
+    load(clampc(c_beg + 1), set1);
+    load(clampc(c_beg + 2), set0);
+    auto iter = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
+      const bool nxt = c + 1 < c_end;
+      if (c < c_end) mfma_chunk(lds[c & 1], lds[(c + 1) & 1], nxt, SETc);
+      load(clampc(c + 3), SETc);
+      __syncthreads();
+    };
+    for (int64_t c = c_beg; c < c_end; c += 2) {
+      iter(c, set1);
+      iter(c + 1, set0);
+    }
+  }
+  if (gmax >= 65504.0f) atomicOr(guard, 1u);
+  if (do_cs) {  // (block-uniform) the bias gradient's column sums: the 8 pixel rows of each co quad, in order
+    csred[tid] = csum;
+    __syncthreads();
+    if (tid < 32) {
+      f32x4 t = csred[tid];
+      for (int r = 1; r < WW_NT / 32; ++r) t += csred[tid + 32 * r];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) colpart[(size_t)zs * a.cout + 4 * tid + j] = t[j];
+    }
+  }
+  // C[i][j] of MFMA tile (ti, tj): co = 64 (wave & 1) + 32 ti + 8 (r >> 2) + 4 h + (r & 3), ci = ci0 + 64 (wave >> 1)
+  // + 32 tj + l32; slab [z][cout][cin]
+  float* slab = a.part + (size_t)zs * a.cout * cin;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj) {
+      const int ci = ci0 + 64 * (wave >> 1) + 32 * tj + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = 64 * (wave & 1) + 32 * ti + 8 * (r >> 2) + 4 * h + (r & 3);
+        slab[(size_t)co * cin + ci] = acc[ti][tj][r];
+      }
+    }
+}
+
 // Warp-specialised 3x3 weight gradient (3xf16 / f16): wgrad_x3_kernel<9, ..>'s arithmetic, LDS image and
 // fragment reads, with the roles split. 8 waves, two per SIMD: waves 0-3 are consumers (quadrant w:
 // 32 co x 32 ci of all 9 taps, 144 accumulator registers), waves 4-7 producers (global loads, the
@@ -2662,11 +2842,25 @@ int ifd_tr_scale(float* x, int64_t n, float s, void* stream) {
 }
 
 // split-K count of wgrad9_kernel: blocks (tiles x splits) >= ~2 per CU, >= 8 chunks per split
-int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* splits) {
+// pixel splits of the 64 x 64-tile weight-gradient kernels
+static int wgrad_splits(int cout, int cin, int64_t P) {
   const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64);
   const int64_t nch = P / 32;
   int S = 1;
   while (S < 1024 && (int64_t)tiles * S < 512 && nch / (2 * S) >= 8) S *= 2;
+  return S;
+}
+// pixel splits of wgrad1x1_wide_kernel: one block per CU (256) over the cin / 128 channel tiles, >= 8 chunks each
+static int ww_splits(int cin, int64_t P) {
+  const int64_t nch = P / WW_PX;
+  int64_t S = 256 / (cin / 128);
+  if (S > nch / 8) S = nch / 8;
+  return S < 1 ? 1 : (int)S;
+}
+
+int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* splits) {
+  int S = wgrad_splits(cout, cin, P);
+  if (taps == 1 && ww_shape(cout, cin) && ww_splits(cin, P) > S) S = ww_splits(cin, P);  // (the larger plan)
   if (splits) *splits = S;
   return (int64_t)S * cout * cin * taps;
 }
@@ -2676,8 +2870,8 @@ int ifd_tr_conv_wgrad(const float* dy, int cout, const float* x0, int c0, const 
                       int64_t colpart_floats, void* stream) {
   const int cin = c0 + c1;
   const int64_t P = (int64_t)N * H * H;
-  int S = 1;
-  const int64_t need = ifd_tr_wgrad_part_floats(cout, cin, taps, P, &S);
+  const int S = wgrad_splits(cout, cin, P);
+  const int64_t need = (int64_t)S * cout * cin * taps;
   if (!dy || !x0 || !dw || !part || need > part_floats || c0 % 4 || (taps != 1 && taps != 9)) {
     set_error("ifd_tr_conv_wgrad: bad arguments or workspace too small");
     return 2;
@@ -2759,8 +2953,11 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
                         void* stream) {
   const int64_t P = (int64_t)N * H * H;
   const int cin = c0 + c1;
-  int S = 1;
-  const int64_t need = ifd_tr_wgrad_part_floats(cout, cin, taps, P, &S);
+  // 1x1 with 128 output channels over 128-channel input tiles (each inside one concat source): the wide kernel
+  const bool wide = taps == 1 && !actA && ww_shape(cout, cin) && (!c1 || (c0 % 128 == 0 && c1 % 128 == 0)) &&
+                    (H * H) % WW_PX == 0;
+  const int S = wide ? ww_splits(cin, P) : wgrad_splits(cout, cin, P);
+  const int64_t need = (int64_t)S * cout * cin * taps;
   if (!dy || !x0 || !dw || !part || need > part_floats || (nprod != 1 && nprod != 3)) {
     set_error("ifd_tr_conv_wgrad_x3: bad arguments or workspace too small");
     return 2;
@@ -2771,7 +2968,7 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
   a.part = part;
   a.actA = actA; a.actB = actB;
   hipStream_t s = (hipStream_t)stream;
-  const int64_t nch = P / WX_PX;
+  const int64_t nch = P / (wide ? WW_PX : WX_PX);
   a.chunks_per_split = (int)((nch + S - 1) / S);
   const int tiles = ((cout + 63) / 64) * ((cin + 63) / 64);
   // bias gradient fused into the kernel when the column-sum workspace holds one row per split
@@ -2779,6 +2976,7 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
   float* cp = fused_db ? colpart : nullptr;
   const bool gna = actA != nullptr;
   const dim3 g9(tiles, S), b1(WxCfg<1>::NT);
+  const dim3 gw(cin / 128, S);
   // 3x3: the warp-specialised kernel (wgrad_x3_kernel<9, ..> measured 1.98 vs 1.79 ms at 256^2 128 -> 128,
   // profiles/r04b/wgrad_exp); 1x1: wgrad_x3_kernel<1, ..>
   if (taps == 9) {
@@ -2790,7 +2988,11 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
       hipLaunchKernelGGL((wgrad_ws_kernel<1, true>), g9, dim3(512), 0, s, a, guard, cp);
     else
       hipLaunchKernelGGL((wgrad_ws_kernel<1, false>), g9, dim3(512), 0, s, a, guard, cp);
-  } else if (nprod == 3)
+  } else if (wide && nprod == 3)
+    hipLaunchKernelGGL((wgrad1x1_wide_kernel<3>), gw, dim3(WW_NT), 0, s, a, guard, cp);
+  else if (wide)
+    hipLaunchKernelGGL((wgrad1x1_wide_kernel<1>), gw, dim3(WW_NT), 0, s, a, guard, cp);
+  else if (nprod == 3)
     hipLaunchKernelGGL((wgrad_x3_kernel<3>), g9, b1, 0, s, a, guard, cp);
   else
     hipLaunchKernelGGL((wgrad_x3_kernel<1>), g9, b1, 0, s, a, guard, cp);

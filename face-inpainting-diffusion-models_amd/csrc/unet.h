@@ -176,6 +176,7 @@ class Model {
   void fill_opts(ConvParams& p) const {
     p.opt_bm128 = 0;
     p.opt_invariant = opt_invariant_;
+    p.opt_img8_partial = 1;
   }
   const float* pooled_raw_ = nullptr;  // tensor whose raw 2x2 pool sits in o_pool2_ (act_pool)
   int prec_ = 0;

@@ -415,43 +415,3 @@ def test_gn_bwd_split_output(N, H, C0, C1):
     with pytest.raises(RuntimeError):
         L.check(lib().ifd_tr_gn_bwd_cat(P(dout), P(xa), C0, P(xb), N, H * H, C, P(gam), P(bet), None, 0, 1, P(st),
                                         P(d0), 1, P(dg), P(db), None, P(work), work.numel(), None, 0, P(d1), s))
-
-
-@pytest.mark.parametrize("N,C", [(1, 256), (2, 256), (3, 512), (2, 128)])
-def test_conv_x3_partial_image_tiles(N, C, record):
-    """The split kernel's four-image 8x8 tiles at N % 4 != 0 through the training entry (GroupNorm + SiLU prologue,
-    residual, split-K statistics) on tensors that are allocations of their own: a spare slot of a partial tile
-    recomputes the batch's last image from a tile origin below 0, and its padding pixels must still read inside
-    the batch (they read below the tensor before, and faulted where that memory was unmapped). Against a float64
-    conv of the materialised activation."""
-    from ifd import _lib
-    from ifd.train import P, chk, lib
-
-    s = _lib.stream_ptr(DEV)
-    H = 8
-    g = torch.Generator().manual_seed(3 + N + C)
-    x = (torch.randn(N, H, H, C, generator=g) + 0.3).to(DEV)
-    res = torch.randn(N, H, H, C, generator=g).to(DEV)
-    w = (torch.randn(C, C, 3, 3, generator=g) / (3 * C ** 0.5)).to(DEV)
-    b = (0.3 * torch.randn(C, generator=g)).to(DEV)
-    A = (1 + 0.1 * torch.randn(N, C, generator=g)).to(DEV)
-    B = (0.1 * torch.randn(N, C, generator=g)).to(DEV)
-    guard = torch.zeros(4, device=DEV, dtype=torch.int32)
-    wx3 = torch.empty(C * C * 9, device=DEV)
-    chk(lib().ifd_tr_pack_conv_x3(P(w), C, C, 9, C, C, 0, P(wx3), P(guard), s))
-    pf = lib().ifd_tr_conv_x3_part_floats(N, H, C, C)
-    part = torch.empty(max(pf, 1), device=DEV)
-    gf = lib().ifd_tr_gstat_floats(N, H, C)
-    gstat = torch.empty(max(gf, 1), device=DEV)
-    out = torch.empty(N, H, H, C, device=DEV)
-    E, cnt = ctypes.c_int(0), ctypes.c_float(0.0)
-    chk(lib().ifd_tr_conv_x3_gn(P(x), C, None, 0, N, H, P(wx3), P(b), C, C, P(A), P(B), P(res), P(out), P(part), pf,
-                                P(guard), P(gstat), gf, ctypes.byref(E), ctypes.byref(cnt), 3, s))
-    torch.cuda.synchronize()
-    assert int(guard.max()) == 0
-    a = torch.nn.functional.silu(x.double() * A.double()[:, None, None, :] + B.double()[:, None, None, :])
-    ref = torch.nn.functional.conv2d(a.permute(0, 3, 1, 2), w.double(), b.double(), padding=1).permute(0, 2, 3, 1)
-    ref = ref + res.double()
-    err = float((out.double() - ref).abs().max())
-    record(f"train_fuse/conv_x3_partial/{N}x8x{C}", maxabs=err)
-    assert err <= 1e-5 * float(ref.abs().max()), err

@@ -70,3 +70,37 @@ def test_wgrad_x3_vs_fp64(N, H, cin, cout, taps, record):
     record(f"wgrad_x3/{N}x{H}x{cin}->{cout}/t{taps}", rel_x3=rel["x3"], rel_fp32=rel["fp32"], rel_bias=relb)
     assert rel["x3"] <= 2e-6 and rel["x3"] <= 2 * rel["fp32"] + 1e-7, rel
     assert relb <= 1e-6, relb
+
+
+@pytest.mark.parametrize("N,H,c0,c1", [(2, 64, 256, 128), (3, 32, 128, 128), (1, 128, 256, 0)])
+def test_wgrad_wide_1x1_vs_fp64(N, H, c0, c1, record):
+    """The wide-tile 1x1 weight gradient (wgrad1x1_wide_kernel: cout 128 over 128-channel input tiles, the output
+    blocks' skip connections) on a concat input x = cat(x0[c0], x1[c1]) (or one tensor), with the bias gradient's
+    column sums fused (the trainer's column-sum workspace): rel-L2 vs float64 as test_wgrad_x3_vs_fp64."""
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    cout, cin = 128, c0 + c1
+    g = torch.Generator().manual_seed(N * 100 + H + c0)
+    x0 = (torch.randn(N, H, H, c0, generator=g) * 0.8 + 0.2).to(DEV)
+    x1 = (torch.randn(N, H, H, c1, generator=g) * 0.5 - 0.1).to(DEV) if c1 else None
+    dy = torch.randn(N, H, H, cout, generator=g).to(DEV)
+    P_ = N * H * H
+    S = ctypes.c_int()
+    need = lib().ifd_tr_wgrad_part_floats(cout, cin, 1, P_, ctypes.byref(S))
+    part = torch.empty(need, device=DEV)
+    colpart = torch.empty(max((P_ + 1023) // 1024, S.value) * cout, device=DEV)
+    guard = torch.zeros(4, device=DEV, dtype=torch.int32)
+    dw, db = torch.zeros(cout * cin, device=DEV), torch.zeros(cout, device=DEV)
+    chk(lib().ifd_tr_conv_wgrad_x3(P(dy), cout, P(x0), c0, P(x1), c1, N, H, 1, P(dw), P(db), P(part), need,
+                                   P(colpart), colpart.numel(), P(guard), 3, s))
+    torch.cuda.synchronize()
+    assert int(guard.max()) == 0
+    x = torch.cat([x0, x1], -1) if c1 else x0
+    rw, rb = _ref(dy, x, 1)
+    rel = float((dw.view(cout, cin, 1).double() - rw).norm() / rw.norm())
+    relb = float((db.double() - rb).norm() / rb.norm())
+    record(f"wgrad_wide/{N}x{H}x{c0}+{c1}->{cout}", rel_x3=rel, rel_bias=relb)
+    assert rel <= 2e-6, rel
+    assert relb <= 1e-6, relb
