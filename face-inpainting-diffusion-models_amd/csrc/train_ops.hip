@@ -705,7 +705,15 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad1x1_wide_kernel(WgArgs a, unsig
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WW_ST];
   f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop (its last barrier)
   const int cin = a.c0 + a.c1;
-  const int cit = blockIdx.x, zs = blockIdx.y;
+  // (channel tile, pixel split): workgroups go to the 8 XCDs round-robin in launch order, so with a split count
+  // divisible by 8 the channel tiles of one split (the same dY chunks) are put 8 launch slots apart, on one XCD,
+  // where the second reads dY from that XCD's L2 (wgrad_x3_kernel's map)
+  int cit = blockIdx.x, zs = blockIdx.y;
+  if ((gridDim.y & 7) == 0) {
+    const int L = blockIdx.x + blockIdx.y * gridDim.x, j = L >> 3;
+    cit = j % gridDim.x;
+    zs = (j / gridDim.x) * 8 + (L & 7);
+  }
   const int ci0 = cit * 128;
   const bool src1 = a.c1 && ci0 >= a.c0;  // the tile's X source (block-uniform; host: 128-channel tiles in one)
   const float* const xsrc = src1 ? a.x1 : a.x0;

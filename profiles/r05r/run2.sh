@@ -5,7 +5,7 @@
 # bench twice and one traced step
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r05r3; mkdir -p $O
+O=$R/gpurun_out/${TAG:-r05r4}; mkdir -p $O
 cd $R
 for a in; do
   timeout -k 10 60 python -u profiles/r05r/repro2.py $a > $O/conv_${a// /_}.txt 2>&1 || { echo "FAILED at $a"; tail -2 $O/conv_${a// /_}.txt; exit 1; }
