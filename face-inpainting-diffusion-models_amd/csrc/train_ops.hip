@@ -688,11 +688,12 @@ __global__ __launch_bounds__(WxCfg<1>::NT, 1) void wgrad_x3_kernel(WgArgs a, uns
 // algorithmic bytes). Same arithmetic per product as wgrad_x3_kernel (split hi / lo, NPROD f16 products into one
 // fp32 accumulator per output, k-steps of 16 pixels in pixel order, splits summed by slab_bias_reduce_kernel).
 // 4 waves, one 64 co x 64 ci quadrant each (2 x 2 MFMA tiles, one 64-channel LDS plane of each operand);
-// chunks of 32 consecutive pixels (NHWC rows, never across images: HW % 32 == 0), staged pixel-major at
+// chunks of WW_PX consecutive pixels (NHWC rows, never across images: HW % WW_PX == 0), staged pixel-major at
 // wgrad_x3_kernel's 96-f16 pitch and read through ds_read_b64_tr_b16. Chunk c + 1 is staged between chunk
 // c's k-steps, loads go out two chunks ahead (two register sets, as wgrad_x3_kernel).
-constexpr int WW_PX = 32;                    // pixels per chunk (2 k-steps)
-constexpr int WW_PL = WW_PX * WX_P;          // one 64-channel plane of one part: 32 rows at the 96-f16 pitch
+constexpr int WW_PX = 16;                    // pixels per chunk (one k-step)
+constexpr int WW_K = WW_PX / 8;              // staging rows per thread and operand
+constexpr int WW_PL = WW_PX * WX_P;          // one 64-channel plane of one part: WW_PX rows at the 96-f16 pitch
 constexpr int WW_OP = 2 * 2 * WW_PL;         // one operand: [part hi / lo][plane 0 / 1]
 constexpr int WW_ST = 2 * WW_OP;             // one stage: dY then X
 constexpr int WW_NT = 256;
@@ -701,7 +702,7 @@ static_assert(2 * WW_ST * 2 <= 160 * 1024, "two stages fit the LDS");
 __host__ __device__ constexpr bool ww_shape(int cout, int cin) { return cout == 128 && cin % 128 == 0 && cin <= 512; }
 
 template <int NPROD>
-__global__ __launch_bounds__(WW_NT, 1) void wgrad1x1_wide_kernel(WgArgs a, unsigned* guard, float* colpart) {
+__global__ __launch_bounds__(WW_NT, 3) void wgrad1x1_wide_kernel(WgArgs a, unsigned* guard, float* colpart) {
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WW_ST];
   f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop (its last barrier)
   const int cin = a.c0 + a.c1;
@@ -735,30 +736,30 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad1x1_wide_kernel(WgArgs a, unsig
   const bool do_cs = colpart && cit == 0;
   f32x4 csum = {0.f, 0.f, 0.f, 0.f};
   // staging items: channel quad cq = tid & 31 (the same for every item of the thread: one co quad of dY, one ci
-  // quad of X), pixel rows pr + 8 k, k < 4, of each operand
+  // quad of X), pixel rows pr + 8 k, k < WW_K, of each operand
   const int cq = tid & 31, pr = tid >> 5;
   const int pl = cq >> 4, col = 4 * (cq & 15);  // LDS plane (64 channels) and column of the quad
   if (c_beg < c_end) {
-    f32x4 dvs[2][4], xvs[2][4];
+    f32x4 dvs[2][WW_K], xvs[2][WW_K];
     auto load = [&](int64_t c, auto SETc) __attribute__((always_inline)) {
-      f32x4(&dv)[4] = dvs[decltype(SETc)::value];
-      f32x4(&xv)[4] = xvs[decltype(SETc)::value];
+      f32x4(&dv)[WW_K] = dvs[decltype(SETc)::value];
+      f32x4(&xv)[WW_K] = xvs[decltype(SETc)::value];
       const int64_t p0 = c * WW_PX;
       const int n = (int)(p0 / HW), q0 = (int)(p0 - (int64_t)n * HW);  // image, its first pixel (chunks stay in it)
       const rsrc_t rd = mkrsrc(a.dy + (size_t)n * HW * a.cout);
       const rsrc_t rx = mkrsrc(xsrc + (size_t)n * HW * xst);
       const int od = __builtin_amdgcn_readfirstlane(q0 * a.cout * 4), ox = __builtin_amdgcn_readfirstlane(q0 * xst * 4);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < WW_K; ++k) {
         dv[k] = bld4(rd, ((pr + 8 * k) * a.cout + 4 * cq) * 4 + od, 0);
         xv[k] = bld4(rx, ((pr + 8 * k) * xst + xc0 + 4 * cq) * 4 + ox, 0);
       }
     };
     auto store_item = [&](_Float16* L, int it, auto SETc) __attribute__((always_inline)) {
-      const f32x4(&dv)[4] = dvs[decltype(SETc)::value];
-      const f32x4(&xv)[4] = xvs[decltype(SETc)::value];
-      const bool isd = it < 4;
-      const int k = it & 3;
+      const f32x4(&dv)[WW_K] = dvs[decltype(SETc)::value];
+      const f32x4(&xv)[WW_K] = xvs[decltype(SETc)::value];
+      const bool isd = it < WW_K;
+      const int k = isd ? it : it - WW_K;
       const f32x4 v = isd ? dv[k] : xv[k];
       if (isd && do_cs) csum += v;
       unsigned h0, l0, h1, l1;
@@ -806,7 +807,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad1x1_wide_kernel(WgArgs a, unsig
         __builtin_amdgcn_sched_barrier(0);
         if (nxt)  // (block-uniform) chunk c + 1's staging, half of it per k-step
 #pragma unroll
-          for (int it = 4 * st; it < 4 * st + 4; ++it) store_item(Ln, it, SETc);
+          for (int it = 4 * st; it < 4 * st + 4; ++it) store_item(Ln, it, SETc);  // (2 WW_K items over WW_PX / 16 k-steps)
         __builtin_amdgcn_sched_barrier(0);
         if (NPROD == 3) {
 #pragma unroll
@@ -825,7 +826,7 @@ __global__ __launch_bounds__(WW_NT, 1) void wgrad1x1_wide_kernel(WgArgs a, unsig
     const std::integral_constant<int, 1> set1;
     load(c_beg, set0);
 #pragma unroll
-    for (int it = 0; it < 8; ++it) store_item(lds[c_beg & 1], it, set0);
+    for (int it = 0; it < 2 * WW_K; ++it) store_item(lds[c_beg & 1], it, set0);
     __syncthreads();
     // (loads past the block's range re-read its last chunk: every iteration issues the same loads)
     auto clampc = [&](int64_t c) { return c < c_end ? c : c_end - 1; };
@@ -2858,10 +2859,10 @@ static int wgrad_splits(int cout, int cin, int64_t P) {
   while (S < 1024 && (int64_t)tiles * S < 512 && nch / (2 * S) >= 8) S *= 2;
   return S;
 }
-// pixel splits of wgrad1x1_wide_kernel: one block per CU (256) over the cin / 128 channel tiles, >= 8 chunks each
+// pixel splits of wgrad1x1_wide_kernel: three blocks per CU (768) over the cin / 128 channel tiles, >= 8 chunks each
 static int ww_splits(int cin, int64_t P) {
   const int64_t nch = P / WW_PX;
-  int64_t S = 256 / (cin / 128);
+  int64_t S = 768 / (cin / 128);  // three blocks per CU (48 KB of LDS each)
   if (S > nch / 8) S = nch / 8;
   return S < 1 ? 1 : (int)S;
 }
