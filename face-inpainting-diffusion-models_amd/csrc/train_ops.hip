@@ -681,11 +681,10 @@ __global__ __launch_bounds__(WxCfg<1>::NT, 1) void wgrad_x3_kernel(WgArgs a, uns
   }
 }
 
-// Wide-tile 1x1 weight gradient (the output blocks' skip connections at 128^2 / 256^2: cout = 128 over a 256- or
-// 384-channel concat): dW[co][ci] = sum_p dY[p][co] X[p][ci] for a 128 co x 128 ci tile per block, so a layer's
-// X is read once and dY once per 128 input channels (wgrad_x3_kernel's 64 x 64 tiles read X cout / 64 and dY
-// cin / 64 times, and staged 0.67 KB per MFMA: 1.8 ms for the 256^2 256 -> 128 layer at B = 32, 1.8 TB/s of
-// algorithmic bytes). Same arithmetic per product as wgrad_x3_kernel (split hi / lo, NPROD f16 products into one
+// Wide-tile 1x1 weight gradient (the skip connections, qkv and proj_out: cout and cin multiples of 128):
+// dW[co][ci] = sum_p dY[p][co] X[p][ci] for a 128 co x 128 ci tile per block, so a layer's X is read cout / 128
+// times and dY cin / 128 times (wgrad_x3_kernel's 64 x 64 tiles read them cout / 64 and cin / 64 times, and staged
+// 0.67 KB per MFMA: 1.8 ms for the 256^2 256 -> 128 layer at B = 32, 1.8 TB/s of algorithmic bytes). Same arithmetic per product as wgrad_x3_kernel (split hi / lo, NPROD f16 products into one
 // fp32 accumulator per output, k-steps of 16 pixels in pixel order, splits summed by slab_bias_reduce_kernel).
 // 4 waves, one 64 co x 64 ci quadrant each (2 x 2 MFMA tiles, one 64-channel LDS plane of each operand);
 // chunks of WW_PX consecutive pixels (NHWC rows, never across images: HW % WW_PX == 0), staged pixel-major at
@@ -699,7 +698,7 @@ constexpr int WW_ST = 2 * WW_OP;             // one stage: dY then X
 constexpr int WW_NT = 256;
 static_assert(2 * WW_ST * 2 <= 160 * 1024, "two stages fit the LDS");
 // eligible shapes (the host also needs 128-channel tiles inside one concat source)
-__host__ __device__ constexpr bool ww_shape(int cout, int cin) { return cout == 128 && cin % 128 == 0 && cin <= 512; }
+__host__ __device__ constexpr bool ww_shape(int cout, int cin) { return cout % 128 == 0 && cin % 128 == 0; }
 
 template <int NPROD>
 __global__ __launch_bounds__(WW_NT, 3) void wgrad1x1_wide_kernel(WgArgs a, unsigned* guard, float* colpart) {
@@ -709,13 +708,14 @@ __global__ __launch_bounds__(WW_NT, 3) void wgrad1x1_wide_kernel(WgArgs a, unsig
   // (channel tile, pixel split): workgroups go to the 8 XCDs round-robin in launch order, so with a split count
   // divisible by 8 the channel tiles of one split (the same dY chunks) are put 8 launch slots apart, on one XCD,
   // where the second reads dY from that XCD's L2 (wgrad_x3_kernel's map)
-  int cit = blockIdx.x, zs = blockIdx.y;
+  int tile = blockIdx.x, zs = blockIdx.y;
   if ((gridDim.y & 7) == 0) {
     const int L = blockIdx.x + blockIdx.y * gridDim.x, j = L >> 3;
-    cit = j % gridDim.x;
+    tile = j % gridDim.x;
     zs = (j / gridDim.x) * 8 + (L & 7);
   }
-  const int ci0 = cit * 128;
+  const int nci = cin / 128, cit = tile % nci;
+  const int ci0 = cit * 128, co0 = (tile / nci) * 128;
   const bool src1 = a.c1 && ci0 >= a.c0;  // the tile's X source (block-uniform; host: 128-channel tiles in one)
   const float* const xsrc = src1 ? a.x1 : a.x0;
   const int xst = src1 ? a.c1 : a.c0, xc0 = src1 ? ci0 - a.c0 : ci0;
@@ -751,7 +751,7 @@ __global__ __launch_bounds__(WW_NT, 3) void wgrad1x1_wide_kernel(WgArgs a, unsig
       const int od = __builtin_amdgcn_readfirstlane(q0 * a.cout * 4), ox = __builtin_amdgcn_readfirstlane(q0 * xst * 4);
 #pragma unroll
       for (int k = 0; k < WW_K; ++k) {
-        dv[k] = bld4(rd, ((pr + 8 * k) * a.cout + 4 * cq) * 4 + od, 0);
+        dv[k] = bld4(rd, ((pr + 8 * k) * a.cout + co0 + 4 * cq) * 4 + od, 0);
         xv[k] = bld4(rx, ((pr + 8 * k) * xst + xc0 + 4 * cq) * 4 + ox, 0);
       }
     };
@@ -851,7 +851,7 @@ __global__ __launch_bounds__(WW_NT, 3) void wgrad1x1_wide_kernel(WgArgs a, unsig
       f32x4 t = csred[tid];
       for (int r = 1; r < WW_NT / 32; ++r) t += csred[tid + 32 * r];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) colpart[(size_t)zs * a.cout + 4 * tid + j] = t[j];
+      for (int j = 0; j < 4; ++j) colpart[(size_t)zs * a.cout + co0 + 4 * tid + j] = t[j];
     }
   }
   // C[i][j] of MFMA tile (ti, tj): co = 64 (wave & 1) + 32 ti + 8 (r >> 2) + 4 h + (r & 3), ci = ci0 + 64 (wave >> 1)
@@ -864,7 +864,7 @@ __global__ __launch_bounds__(WW_NT, 3) void wgrad1x1_wide_kernel(WgArgs a, unsig
       const int ci = ci0 + 64 * (wave >> 1) + 32 * tj + (lane & 31);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = 64 * (wave & 1) + 32 * ti + 8 * (r >> 2) + 4 * h + (r & 3);
+        const int co = co0 + 64 * (wave & 1) + 32 * ti + 8 * (r >> 2) + 4 * h + (r & 3);
         slab[(size_t)co * cin + ci] = acc[ti][tj][r];
       }
     }
@@ -2859,17 +2859,18 @@ static int wgrad_splits(int cout, int cin, int64_t P) {
   while (S < 1024 && (int64_t)tiles * S < 512 && nch / (2 * S) >= 8) S *= 2;
   return S;
 }
-// pixel splits of wgrad1x1_wide_kernel: three blocks per CU (768) over the cin / 128 channel tiles, >= 8 chunks each
-static int ww_splits(int cin, int64_t P) {
+// pixel splits of wgrad1x1_wide_kernel: three blocks per CU (768) over the (cout / 128) (cin / 128) channel tiles,
+// >= 8 chunks each
+static int ww_splits(int cout, int cin, int64_t P) {
   const int64_t nch = P / WW_PX;
-  int64_t S = 768 / (cin / 128);  // three blocks per CU (48 KB of LDS each)
+  int64_t S = 768 / ((cout / 128) * (cin / 128));  // three blocks per CU (48 KB of LDS each)
   if (S > nch / 8) S = nch / 8;
   return S < 1 ? 1 : (int)S;
 }
 
 int64_t ifd_tr_wgrad_part_floats(int cout, int cin, int taps, int64_t P, int* splits) {
   int S = wgrad_splits(cout, cin, P);
-  if (taps == 1 && ww_shape(cout, cin) && ww_splits(cin, P) > S) S = ww_splits(cin, P);  // (the larger plan)
+  if (taps == 1 && ww_shape(cout, cin) && ww_splits(cout, cin, P) > S) S = ww_splits(cout, cin, P);  // (the larger plan)
   if (splits) *splits = S;
   return (int64_t)S * cout * cin * taps;
 }
@@ -2962,10 +2963,10 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
                         void* stream) {
   const int64_t P = (int64_t)N * H * H;
   const int cin = c0 + c1;
-  // 1x1 with 128 output channels over 128-channel input tiles (each inside one concat source): the wide kernel
+  // 1x1 over 128 x 128 channel tiles (each input tile inside one concat source): the wide kernel
   const bool wide = taps == 1 && !actA && ww_shape(cout, cin) && (!c1 || (c0 % 128 == 0 && c1 % 128 == 0)) &&
                     (H * H) % WW_PX == 0;
-  const int S = wide ? ww_splits(cin, P) : wgrad_splits(cout, cin, P);
+  const int S = wide ? ww_splits(cout, cin, P) : wgrad_splits(cout, cin, P);
   const int64_t need = (int64_t)S * cout * cin * taps;
   if (!dy || !x0 || !dw || !part || need > part_floats || (nprod != 1 && nprod != 3)) {
     set_error("ifd_tr_conv_wgrad_x3: bad arguments or workspace too small");
@@ -2985,7 +2986,7 @@ static int wgrad_x3_run(const float* dy, int cout, const float* x0, int c0, cons
   float* cp = fused_db ? colpart : nullptr;
   const bool gna = actA != nullptr;
   const dim3 g9(tiles, S), b1(WxCfg<1>::NT);
-  const dim3 gw(cin / 128, S);
+  const dim3 gw((cout / 128) * (cin / 128), S);
   // 3x3: the warp-specialised kernel (wgrad_x3_kernel<9, ..> measured 1.98 vs 1.79 ms at 256^2 128 -> 128,
   // profiles/r04b/wgrad_exp); 1x1: wgrad_x3_kernel<1, ..>
   if (taps == 9) {

@@ -72,17 +72,18 @@ def test_wgrad_x3_vs_fp64(N, H, cin, cout, taps, record):
     assert relb <= 1e-6, relb
 
 
-@pytest.mark.parametrize("N,H,c0,c1", [(2, 64, 256, 128), (3, 32, 128, 128), (1, 128, 256, 0)])
-def test_wgrad_wide_1x1_vs_fp64(N, H, c0, c1, record):
-    """The wide-tile 1x1 weight gradient (wgrad1x1_wide_kernel: cout 128 over 128-channel input tiles, the output
-    blocks' skip connections) on a concat input x = cat(x0[c0], x1[c1]) (or one tensor), with the bias gradient's
+@pytest.mark.parametrize("N,H,c0,c1,cout", [(2, 64, 256, 128, 128), (3, 32, 128, 128, 128), (1, 128, 256, 0, 128),
+                                             (2, 16, 512, 0, 1536), (4, 16, 256, 256, 256)])
+def test_wgrad_wide_1x1_vs_fp64(N, H, c0, c1, cout, record):
+    """The wide-tile 1x1 weight gradient (wgrad1x1_wide_kernel: 128 x 128 channel tiles; the skip connections, the
+    qkv 512 -> 1536 and proj_out) on a concat input x = cat(x0[c0], x1[c1]) (or one tensor), with the bias gradient's
     column sums fused (the trainer's column-sum workspace): rel-L2 vs float64 as test_wgrad_x3_vs_fp64."""
     from ifd import _lib
     from ifd.train import P, chk, lib
 
     s = _lib.stream_ptr(DEV)
-    cout, cin = 128, c0 + c1
-    g = torch.Generator().manual_seed(N * 100 + H + c0)
+    cin = c0 + c1
+    g = torch.Generator().manual_seed(N * 100 + H + c0 + cout)
     x0 = (torch.randn(N, H, H, c0, generator=g) * 0.8 + 0.2).to(DEV)
     x1 = (torch.randn(N, H, H, c1, generator=g) * 0.5 - 0.1).to(DEV) if c1 else None
     dy = torch.randn(N, H, H, cout, generator=g).to(DEV)
