@@ -2838,6 +2838,74 @@ int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, 
                      nullptr, 0, nullptr, nullptr, nprod, stream, nullptr, nullptr, &g, gpart_nsl);
 }
 
+// 1x1 conv (forward, or transpose = 1: the dgrad W^T) on the sampler's dedicated split 1x1 kernel (skip_x3.hip,
+// HBM-bound, its weight tile resident in LDS), with the weights packed on the device into its layout
+// [cout/ntc][K/16][part][h][ntc][8] f16 - unet.hip pack_skip1x1_x3's arithmetic (hi = f16(v), part 0 = f16(hi 2^11),
+// part 1 = f16((v - hi) 2^11); a part-0 value outside the f16 range sets the guard). The training step's 1x1
+// convs at 256^2 ran ~1 ms each on the split conv kernel's 1x1 chunks.
+__global__ void pack_skip1x1_kernel(const float* __restrict__ w, int wcout, int wcin, int transpose, int ntc, int K,
+                                    _Float16* __restrict__ dst, unsigned* guard) {
+  const int co_n = transpose ? wcin : wcout;  // output channels of the conv
+  const int64_t tot = (int64_t)co_n * K * 2;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int j = (int)(i & 7);
+  int64_t r = i >> 3;
+  const int col = (int)(r % ntc);
+  r /= ntc;
+  const int hh = (int)(r & 1);
+  r >>= 1;
+  const int part = (int)(r & 1);
+  r >>= 1;
+  const int ksn = K / 16;
+  const int ks = (int)(r % ksn), nt = (int)(r / ksn);
+  const int co = nt * ntc + col, ci = ks * 16 + hh * 8 + j;
+  const int kin = transpose ? wcout : wcin;
+  const float v = ci < kin ? (transpose ? w[(int64_t)ci * wcin + co] : w[(int64_t)co * wcin + ci]) : 0.f;
+  const _Float16 hi = (_Float16)v;
+  _Float16 o;
+  if (part == 0) {
+    const float sc = (float)hi * 2048.0f;
+    if (!(fabsf(sc) <= 65504.0f)) atomicOr(guard, 1u);
+    o = (_Float16)sc;
+  } else {
+    o = (_Float16)((v - (float)hi) * 2048.0f);
+  }
+  dst[i] = o;
+}
+
+int64_t ifd_tr_conv1x1_pack_floats(int cout, int cin, int transpose) {
+  return (int64_t)(transpose ? cin : cout) * (transpose ? cout : cin);
+}
+
+int ifd_tr_conv1x1_x3(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* w, int cout, int cin,
+                      int transpose, const float* bias, float* out, void* wpack, int64_t wpack_floats, unsigned* guard,
+                      int nprod, void* stream) {
+  const int co_n = transpose ? cin : cout, K = c0 + c1;
+  Skip1x1Params q{};
+  q.s0 = x0; q.sc0 = c0; q.s1 = c1 ? x1 : nullptr; q.sc1 = c1;
+  q.npix = N * H * H;
+  q.cout = co_n;
+  q.wpack = wpack; q.bias = bias; q.out = out; q.guard = guard;
+  q.ntc = skip_x3_ntc(K, co_n);
+  q.nprod = nprod;
+  if (!w || !bias || !out || !wpack || !guard || !x0 || K != (transpose ? cout : cin) || !skip_x3_eligible(q) ||
+      ifd_tr_conv1x1_pack_floats(cout, cin, transpose) > wpack_floats) {
+    set_error("ifd_tr_conv1x1_x3: shape not eligible for the split 1x1 kernel (use ifd_tr_conv_x3_taps)");
+    return 3;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t tot = (int64_t)co_n * K * 2;
+  hipLaunchKernelGGL(pack_skip1x1_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, w, cout, cin, transpose,
+                     q.ntc, K, (_Float16*)wpack, guard);
+  const int e = launch_skip_x3(q, s);
+  if (e) {
+    set_error(std::string("ifd_tr_conv1x1_x3: launch failed: ") + hipGetErrorString((hipError_t)e));
+    return 1;
+  }
+  return TR_LAST();
+}
+
 int64_t ifd_tr_gstat_floats(int N, int H, int cout) {
   const int64_t HW = (int64_t)H * H;
   const int64_t E = HW >= 64 ? HW / 64 : 1;

@@ -40,6 +40,8 @@ TRAIN_EXPORTS = {
     "ifd_tr_conv_x3_part_floats": (i64, [i32, i32, i32, i32]),
     "ifd_tr_conv_x3": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, vp]),
     "ifd_tr_conv_x3_taps": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, i32, vp]),
+    "ifd_tr_conv1x1_pack_floats": (i64, [i32, i32, i32]),
+    "ifd_tr_conv1x1_x3": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, i32, i32, vp, vp, vp, i64, vp, i32, vp]),
     "ifd_tr_gstat_floats": (i64, [i32, i32, i32]),
     "ifd_tr_conv_x3_gstat": (i32, [vp, i32, vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i32, vp, i64,
                                    vp, vp, i32, vp]),
@@ -383,12 +385,38 @@ class UNetTrainer:
                 return out
         return self.conv(x, cin, N, H, "out.2.weight", "out.2.bias", gn=gn)
 
+    # the dedicated split 1x1 kernel from this resolution up (the sampler's skip_sep threshold: below it the split
+    # conv kernel's 1x1 chunks keep more of the chip busy)
+    CONV1X1_MIN_H = 64
+
+    def _conv1x1_x3(self, x, cin_x, N, H, name, bias_name, res, x1, c1, transpose, gn):
+        """A 1x1 conv (skip_connection forward / dgrad) without residual or prologue on ifd_tr_conv1x1_x3
+        (skip_x3.hip, weights packed on the device each call); None when it does not take the shape."""
+        w = self.p(name)
+        if w.dim() != 4 or tuple(w.shape[2:]) != (1, 1) or res is not None or gn is not None or H < self.CONV1X1_MIN_H:
+            return None
+        cout, cin = w.shape[0], w.shape[1]
+        co = cin if transpose else cout
+        if cin_x + c1 != (cout if transpose else cin) or co % 4:
+            return None
+        wp = self._empty(max(lib().ifd_tr_conv1x1_pack_floats(cout, cin, int(transpose)), 1))
+        b = self.p(bias_name) if bias_name else self._zero_bias
+        out = self._empty(N, H, H, co)
+        rc = lib().ifd_tr_conv1x1_x3(P(x), cin_x, P(x1), c1, N, H, P(w), cout, cin, int(transpose), P(b), P(out), P(wp),
+                                     wp.numel(), P(self._guard), self._nprod(), self.s)
+        if rc == 3:
+            return None
+        chk(rc)
+        return out
+
     def conv(self, x, cin_x, N, H, name, bias_name=None, res=None, x1=None, c1=0, transpose=False, gn=None):
         """NHWC conv of concat(x[cin_x], x1[c1]) with weight `name` (forward or, transposed, dgrad).
         Output channels are padded to a multiple of 4 (zero weight rows): the 6-channel head writes 8.
         gn = (A, B): the conv's input is silu(A x + B) of the raw x (fuse_gn), applied on load."""
         if self._x3_active(transpose):
-            out = self._conv_x3(x, cin_x, N, H, name, bias_name, res, x1, c1, transpose, gn=gn)
+            out = self._conv1x1_x3(x, cin_x, N, H, name, bias_name, res, x1, c1, transpose, gn)
+            if out is None:
+                out = self._conv_x3(x, cin_x, N, H, name, bias_name, res, x1, c1, transpose, gn=gn)
             if out is not None:
                 return out
         buf, pout, pin, taps, bn, cin_pad, cout_pad = self._packed(name, int(transpose))

@@ -186,6 +186,15 @@ int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const fl
                             const float* stats, const float* part, int part_nsl, float* dx, int accumulate,
                             float* dgamma, float* dbeta, float* dss, float* work, int64_t work_floats, const float* add,
                             int add_stride, float* dx1, void* stream);
+/* 1x1 conv out[px][co] = bias[co] + sum_k W[co][k] cat(x0[c0], x1[c1])[px][k] (code/nn.py:184 skip_connection,
+ * and its dgrad with transpose = 1: W^T, cout <-> cin) on the dedicated split 1x1 kernel (the sampler's
+ * skip_x3.hip), the weights W[cout][cin] packed on the device into wpack (ifd_tr_conv1x1_pack_floats floats).
+ * Returns 3 when the shape is not eligible (c0, c1 multiples of 16, c0 + c1 a multiple of 64, N*H*H a multiple of
+ * 32): the caller uses ifd_tr_conv_x3_taps. nprod 3 (3xf16) or 1 (f16). */
+int64_t ifd_tr_conv1x1_pack_floats(int cout, int cin, int transpose);
+int ifd_tr_conv1x1_x3(const float* x0, int c0, const float* x1, int c1, int N, int H, const float* w, int cout, int cin,
+                      int transpose, const float* bias, float* out, void* wpack, int64_t wpack_floats, unsigned* guard,
+                      int nprod, void* stream);
 /* nearest-up x2 (mode 1) / AvgPool2d(2) (mode 2) (code/nn.py:92-133) and the adjoint (dx at Hin). */
 int ifd_tr_resample(const float* x, int N, int Hin, int C, int mode, float* out, void* stream);
 int ifd_tr_resample_bwd(const float* dy, int N, int Hin, int C, int mode, float* dx, int accumulate, void* stream);

@@ -415,3 +415,36 @@ def test_gn_bwd_split_output(N, H, C0, C1):
     with pytest.raises(RuntimeError):
         L.check(lib().ifd_tr_gn_bwd_cat(P(dout), P(xa), C0, P(xb), N, H * H, C, P(gam), P(bet), None, 0, 1, P(st),
                                         P(d0), 1, P(dg), P(db), None, P(work), work.numel(), None, 0, P(d1), s))
+
+
+@pytest.mark.parametrize("N,H,c0,c1,cout,transpose", [(2, 64, 128, 128, 128, 0), (2, 64, 128, 0, 256, 1),
+                                                      (1, 64, 256, 128, 128, 0), (3, 32, 64, 0, 128, 0)])
+def test_conv1x1_x3_vs_fp64(N, H, c0, c1, cout, transpose, record):
+    """ifd_tr_conv1x1_x3: the training step's 1x1 convs (skip_connection forward over the output blocks' concat,
+    and its dgrad through W^T) on the dedicated split 1x1 kernel with the device-side weight packing, against a
+    float64 reference (transpose: the input has cout channels, the output cin = c0)."""
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    g = torch.Generator().manual_seed(N + H + c0 + cout + transpose)
+    # the weight W[wcout][wcin]; transpose: the dgrad maps the conv's wcout-channel gradient (here x) to wcin = cout
+    wcout, wcin = (c0 + c1, cout) if transpose else (cout, c0 + c1)
+    w = (torch.randn(wcout, wcin, generator=g) / 16).to(DEV)
+    x0 = torch.randn(N, H, H, c0, generator=g).to(DEV)
+    x1 = torch.randn(N, H, H, c1, generator=g).to(DEV) if c1 else None
+    co = wcin if transpose else wcout
+    b = (0.1 * torch.randn(co, generator=g)).to(DEV)
+    guard = torch.zeros(4, device=DEV, dtype=torch.int32)
+    wp = torch.empty(lib().ifd_tr_conv1x1_pack_floats(wcout, wcin, transpose), device=DEV)
+    out = torch.empty(N, H, H, co, device=DEV)
+    chk(lib().ifd_tr_conv1x1_x3(P(x0), c0, P(x1), c1, N, H, P(w), wcout, wcin, transpose, P(b), P(out), P(wp),
+                                wp.numel(), P(guard), 3, s))
+    torch.cuda.synchronize()
+    assert int(guard.max()) == 0
+    x = torch.cat([x0, x1], -1) if c1 else x0
+    wm = w.double().t() if transpose else w.double()  # [co][k]
+    ref = x.double() @ wm.t() + b.double()
+    err = float((out.double() - ref).abs().max())
+    record(f"train_fuse/conv1x1_x3/{N}x{H}x{c0}+{c1}->{co}/t{transpose}", maxabs=err)
+    assert err <= 2e-6 * float(ref.abs().max()), err
