@@ -11,6 +11,7 @@ namespace ifd {
 static thread_local std::string g_err;
 void set_error(const std::string& m) { g_err = m; }
 const char* get_error() { return g_err.c_str(); }
+void clear_error() { g_err.clear(); }
 }  // namespace ifd
 
 struct ifd_handle {
@@ -22,6 +23,7 @@ using ifd::set_error;
 extern "C" {
 
 const char* ifd_last_error(void) { return ifd::get_error(); }
+void ifd_clear_error(void) { ifd::clear_error(); }
 const char* ifd_version(void) { return "ifd 0.2 gfx950 fp32-mfma + 3xf16-split-mfma"; }
 
 int ifd_create(const ifd_config* cfg, ifd_handle** out) {
@@ -184,9 +186,7 @@ static int update_common(int mode, const float* out6, int64_t B, int H, int W, f
   ifd::StepCoeffs sc;
   std::memcpy(&sc, c, sizeof(sc));
   ifd::launch_step(mode, sc, out6, img, gt, mask, noise, known, (int)B, H * W, (hipStream_t)stream);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return 1; }
-  return 0;
+  return ifd::launch_status(mode == ifd::EPI_DDPM ? "ifd_ddpm_update" : "ifd_ddim_update") ? 1 : 0;
 }
 
 int ifd_ddim_update(const float* out6, int64_t B, int H, int W, float* img, const float* gt, const float* mask,
@@ -203,9 +203,7 @@ int ifd_blend(const float* result, const float* gt, const float* mask, int64_t B
               void* stream) {
   if (!result || !gt || !mask || !out) { set_error("ifd_blend: null argument"); return 2; }
   ifd::launch_blend(result, gt, mask, out, (int)B, C, H * W, (hipStream_t)stream);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return 1; }
-  return 0;
+  return IFD_LAUNCH_STATUS() ? 1 : 0;
 }
 
 int ifd_to_u8(const float* sample, int64_t B, int C, int H, int W, uint8_t* out_nhwc, void* stream) {
@@ -213,18 +211,14 @@ int ifd_to_u8(const float* sample, int64_t B, int C, int H, int W, uint8_t* out_
   if (B == 0) return 0;  /* an empty tensor may carry a null pointer */
   if (!sample || !out_nhwc) { set_error("ifd_to_u8: null argument"); return 2; }
   ifd::launch_to_u8(sample, out_nhwc, (int)B, C, H * W, (hipStream_t)stream);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return 1; }
-  return 0;
+  return IFD_LAUNCH_STATUS() ? 1 : 0;
 }
 
 int ifd_mask_from_gray(const uint8_t* gray, int64_t n, float* mask, void* stream) {
   if (n < 0 || ((!gray || !mask) && n > 0)) { set_error("ifd_mask_from_gray: bad argument"); return 2; }
   if (n == 0) return 0;
   ifd::launch_mask_from_gray(gray, mask, n, (hipStream_t)stream);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return 1; }
-  return 0;
+  return IFD_LAUNCH_STATUS() ? 1 : 0;
 }
 
 }  // extern "C"

@@ -11,6 +11,31 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 void set_error(const std::string& msg);
 const char* get_error();
+void clear_error();
+
+// The status of the launch just issued (hipGetLastError), with the error message set for it, naming `where`
+// (callers pass __func__), so a nonzero status never reaches the host with another call's message. A fault of
+// an EARLIER asynchronous launch (illegal address, ...) surfaces at the next launch check: the message says so.
+inline int launch_status(const char* where) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    std::string m = std::string(where) + ": " + hipGetErrorString(e);
+    if (e == hipErrorIllegalAddress || e == hipErrorLaunchFailure || e == hipErrorAssert)
+      m += " (a device fault; it may come from an earlier asynchronous launch on this device)";
+    set_error(m);
+  }
+  return (int)e;
+}
+#define IFD_LAUNCH_STATUS() ::ifd::launch_status(__func__)
+// A failed launcher status inside a host routine: the message names what was running and the HIP status.
+#define IFD_LAUNCH_OK(e, what)                                                           \
+  do {                                                                                   \
+    if ((e) != 0) {                                                                      \
+      ::ifd::set_error(std::string("ifd: ") + (what) + " launch: " +                     \
+                       hipGetErrorString((hipError_t)(e)));                             \
+      return (e);                                                                        \
+    }                                                                                    \
+  } while (0)
 
 #define IFD_CHECK_HIP(expr)                                                              \
   do {                                                                                   \

@@ -86,8 +86,8 @@ struct ConvParams {
   int opt_bm128;  // fp32 kernel: 128-pixel tiles only (the training 1x1 convs)
   int opt_invariant;
   // the split kernel's four-image 8 x 8 tiles at any batch (a partial last tile, conv_x3.hip unit_of): set by
-  // the sampler (unet.h fill_opts); the training ops keep whole tiles (N % 4 == 0): a partial tile faulted in
-  // their reduced-config step (separately allocated tensors), cause not yet isolated
+  // the sampler (unet.h fill_opts) and the training ops (train_ops.hip conv_x3_params). Round 6 fixed the
+  // fault this was gated on: the ACT_NONE coefficient loads read from the moved tile origin, below the tensor.
   int opt_img8_partial;
   // 3xf16 range guard (conv_x3.hip): set to 1 when an operand's magnitude reaches the f16 range
   // (|a| >= 65504 would split into inf). The host re-runs the eval in fp32 when it is set.

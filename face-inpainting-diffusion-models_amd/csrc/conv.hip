@@ -520,7 +520,7 @@ static int launch_inst(const ConvParams& p, size_t lds, hipStream_t stream) {
   const int ptiles = (p.npix_tiles + 7) / 8 * 8;
   dim3 grid(ptiles * (p.cout_pad / BN), 1, p.ksplit);
   hipLaunchKernelGGL((conv_kernel<BM, BN, WGM, WGN, TAPS, XF, MAXI, ONEIMG>), grid, dim3(NT), lds, stream, p);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 template <int BM, int BN, int WGM, int WGN, int TAPS, int XF>
@@ -739,13 +739,13 @@ int launch_splitk_gstat(const ConvParams& p, int* E, float* cnt, hipStream_t str
   *cnt = 4.0f * slice;
   const int nqb = (p.cout / 4 + SKG_Q - 1) / SKG_Q;
   hipLaunchKernelGGL(splitk_gstat_kernel, dim3(*E * nqb, p.N), dim3(256), 0, stream, p);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 int launch_splitk_reduce(const ConvParams& p, hipStream_t stream) {
   const size_t tot = (size_t)p.N * p.H * p.W * p.cout;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, p);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 int launch_conv(const ConvParams& p, int taps, int xform, int bn, hipStream_t stream) {

@@ -480,7 +480,7 @@ int launch_conv_head(const ConvParams& p, const float* wh, hipStream_t stream) {
     hipLaunchKernelGGL(conv_head_kernel<6>, dim3(blocks), dim3(HD_NT), 0, stream, p, wh);
   else
     hipLaunchKernelGGL(conv_head_kernel<3>, dim3(blocks), dim3(HD_NT), 0, stream, p, wh);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 }  // namespace ifd
@@ -559,7 +559,7 @@ int launch_pack_head_x3(const float* w, int cout, int cin, float* dst, unsigned*
   const int64_t tot = (int64_t)(cin / HX_CH) * 9 * 2 * HX_WCO * HX_CH;
   hipLaunchKernelGGL(pack_head_x3_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, w, cout, cin,
                      reinterpret_cast<_Float16*>(dst), guard);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 namespace {
@@ -571,7 +571,7 @@ int launch_head_ws(const ConvParams& p, const float* wx, int grid, hipStream_t s
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((conv_head_x3ws_kernel<CO, ACT, EPI>), dim3(grid), dim3(HW_NT), HW_LDS, stream, p,
                      reinterpret_cast<const _Float16*>(wx));
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 template <int CO, int ACT>
 int launch_head_ws_epi(const ConvParams& p, const float* wx, int grid, hipStream_t stream) {

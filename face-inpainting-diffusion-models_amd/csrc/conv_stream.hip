@@ -604,7 +604,7 @@ static int launch_stream_inst(const ConvParams& p, hipStream_t stream) {
   const int nvirt = p.npix_tiles * (p.cout_pad / SBN);
   const int grid = nvirt < ncu ? nvirt : ncu;  // one workgroup per CU (LDS-bound)
   hipLaunchKernelGGL((conv_stream_kernel<XF, CW>), dim3(grid), dim3(64 * CW + NP_T), conv_stream_lds_bytes(), stream, p);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 template <int XF>
@@ -617,7 +617,7 @@ static int launch_stream2_inst(const ConvParams& p, hipStream_t stream) {
   const int nvirt = p.npix_tiles * (p.cout_pad / SBN);
   const int grid = nvirt < 2 * ncu ? nvirt : 2 * ncu;  // two workgroups per CU
   hipLaunchKernelGGL((conv_stream2_kernel<XF>), dim3(grid), dim3(NT), lds, stream, p);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 int launch_conv_stream(const ConvParams& p, int xform, int mode, hipStream_t stream) {

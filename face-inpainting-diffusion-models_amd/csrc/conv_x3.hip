@@ -246,9 +246,13 @@ struct XProducer {
     r0 = mkrsrc(p.in0 + (size_t)t.n0 * img * p.c0);
     r1 = mkrsrc(p.in1 ? p.in1 + (size_t)t.n0 * img * p.c1 : p.in0);
     const int ctot = p.c0 + p.c1;
-    // act == ACT_NONE: the coefficient loads still issue (fixed vmcnt arithmetic) from the input
-    ra = p.actA ? mkrsrc(p.actA + ((size_t)t.n0 + pimg) * ctot) : r0;
-    rb = p.actB ? mkrsrc(p.actB + ((size_t)t.n0 + pimg) * ctot) : r0;
+    // act == ACT_NONE: the coefficient loads still issue (fixed vmcnt arithmetic), from the start of this thread's
+    // own image of the input (offsets < ctot * 4 B). Not from r0: a partial four-image tile moves the tile origin
+    // n0 of its spare slots below image 0 (unit_of), and r0's offset 0 then lies below the tensor (the status-700
+    // fault of the training step's dgrad convs, profiles/r05r/repro4_async.txt).
+    const rsrc_t rself = mkrsrc(p.in0 + ((size_t)t.n0 + pimg) * img * p.c0);
+    ra = p.actA ? mkrsrc(p.actA + ((size_t)t.n0 + pimg) * ctot) : rself;
+    rb = p.actB ? mkrsrc(p.actB + ((size_t)t.n0 + pimg) * ctot) : rself;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int y = t.y0 + hy[i] - 1, x = t.x0 + hx[i] - 1;
@@ -1291,7 +1295,7 @@ static int launch_x3_inst(const ConvParams& p, hipStream_t stream) {
   const int nunit = p.npix_tiles * (p.cout_pad / XBN) * p.ksplit;
   const int grid = nunit < ncu ? nunit : ncu;  // one workgroup per CU (LDS-bound)
   hipLaunchKernelGGL((conv_x3_kernel<XF, SKIP, TW, NPROD>), dim3(grid), dim3(NT), lds, stream, p);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 template <int TW, int NPROD>
@@ -1304,7 +1308,7 @@ static int launch_x3_gnb_inst(const ConvParams& p, const GnbParams& g, hipStream
   const int nunit = p.npix_tiles * (p.cout_pad / XBN) * p.ksplit;
   const int grid = nunit < ncu ? nunit : ncu;
   hipLaunchKernelGGL((conv_x3_gnb_kernel<TW, NPROD>), dim3(grid), dim3(NT), lds, stream, p, g);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 template <int TW, int NPROD>

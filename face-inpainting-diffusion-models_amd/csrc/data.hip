@@ -216,7 +216,7 @@ int ifd_resize_u8(const uint8_t* src, int64_t N, int C, int Hin, int Win, int Ho
   if (!need_h && !need_v) {
     const int64_t n = N * Hin * (int64_t)Win * C;
     hipLaunchKernelGGL(copy_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
-    return (int)hipGetLastError();
+    return IFD_LAUNCH_STATUS();
   }
   DevCoeffs cv, ch;
   if (get_coeffs(Hin, Hout, &cv)) return 1;
@@ -242,7 +242,7 @@ int ifd_resize_u8(const uint8_t* src, int64_t N, int C, int Hin, int Win, int Ho
     hipLaunchKernelGGL(resample_v_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, vin, vrows, Wout, C,
                        Hout, cv.bounds, cv.kk, cv.ksize, yshift, dst, tot);
   }
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 int ifd_image_to_float(const uint8_t* src_nhwc, int64_t N, int C, int H, int W, float* dst_nchw, void* stream) {
@@ -252,7 +252,7 @@ int ifd_image_to_float(const uint8_t* src_nhwc, int64_t N, int C, int H, int W, 
   if (!src_nhwc || !dst_nchw) { set_error("ifd_image_to_float: null argument"); return 2; }
   hipLaunchKernelGGL(image_to_float_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      src_nhwc, C, H * W, dst_nchw, tot);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 int ifd_make_inpaint_batch(const float* images, int64_t N, int H, int W, const uint8_t* mask_bank, int M,
@@ -263,7 +263,7 @@ int ifd_make_inpaint_batch(const float* images, int64_t N, int H, int W, const u
   if (!mask_bank || !idx || (masked_image && !images)) { set_error("ifd_make_inpaint_batch: null argument"); return 2; }
   hipLaunchKernelGGL(inpaint_batch_kernel, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      images, H * W, mask_bank, M, idx, mask, masked_image, npix);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 }  // extern "C"

@@ -91,7 +91,7 @@ int ifd_lib_inject(const float* x, const float* gt, const float* keep, const flo
   if (!x || !gt || !keep || !noise || !out) { set_error("ifd_lib_inject: null argument"); return 2; }
   hipLaunchKernelGGL(lib_inject_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, gt,
                      keep, noise, ca, cb, C, (int64_t)H * W, out, tot);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 int ifd_lib_update(int ddim, const float* x, const float* out6, const float* noise, int64_t B, int H, int W,
@@ -107,7 +107,7 @@ int ifd_lib_update(int ddim, const float* x, const float* out6, const float* noi
   else
     hipLaunchKernelGGL(lib_ddpm_kernel, g, dim3(256), 0, (hipStream_t)stream, x, out6, noise, *c, (int64_t)H * W, sample,
                        pred_xstart, tot);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 }  // extern "C"

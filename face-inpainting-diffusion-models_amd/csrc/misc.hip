@@ -493,7 +493,7 @@ int launch_act_apply(const float* x, int C, int N, int HW, int act, const float*
   const size_t tot = (size_t)N * HW * (C / 4);
   hipLaunchKernelGGL(act_apply_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, x, C, HW, act, A, B, tot,
                      out);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 int launch_act_pool(const float* x, int C, int N, int Hin, int act, const float* A, const float* B, float* out,
@@ -501,7 +501,7 @@ int launch_act_pool(const float* x, int C, int N, int Hin, int act, const float*
   const size_t tot = (size_t)N * (Hin / 2) * (Hin / 2) * (C / 4);
   hipLaunchKernelGGL(act_pool_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, x, C, N, Hin, act, A, B,
                      out, out_raw);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 }  // namespace ifd

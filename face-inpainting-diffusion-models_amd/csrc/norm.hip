@@ -186,7 +186,7 @@ int launch_gn(const float* p0, int c0, const float* p1, int c1, int N, int HW, c
   fp.eps = 1e-5f;
   fp.A = A; fp.B = B;
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(GN_NT), 0, stream, fp);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -380,7 +380,7 @@ int launch_gn_granules(const float* x, int C, int N, int HW, float* part, int* E
   hipLaunchKernelGGL(gn_granules_kernel, dim3(gp.E, N), dim3(GN_NT), 0, stream, gp);
   *E = gp.E;
   *cnt = 4.0f * gp.slice;
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 int launch_gn_finalize2(const float* part0, int E0, float cnt0, int C0, const float* part1, int E1, float cnt1,
@@ -395,7 +395,7 @@ int launch_gn_finalize2(const float* part0, int E0, float cnt0, int C0, const fl
   fp.A = A; fp.B = B;
   IFD_REQUIRE((C0 + C1) % GN_G == 0 && (C0 + C1) / GN_G <= GN_NT, "GroupNorm group width");
   hipLaunchKernelGGL(gn_finalize2_kernel, dim3(GN_G, N), dim3(GN_NT), 0, stream, fp);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 }  // namespace ifd

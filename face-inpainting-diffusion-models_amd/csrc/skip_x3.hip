@@ -248,7 +248,7 @@ int launch_inst(const Skip1x1Params& p, hipStream_t stream) {
   if (per < 1) per = 1;
   if (per > waves_needed) per = waves_needed;
   hipLaunchKernelGGL((skip_x3_kernel<NTC, NPROD>), dim3(per * nnt), dim3(SK_NT), lds, stream, p);
-  return (int)hipGetLastError();
+  return IFD_LAUNCH_STATUS();
 }
 
 }  // namespace

@@ -2535,7 +2535,7 @@ __global__ void scale_kernel(float* __restrict__ x, int64_t n, float s) {
 
 using namespace ifd;
 
-#define TR_LAST() ((int)hipGetLastError())
+#define TR_LAST() IFD_LAUNCH_STATUS()
 
 extern "C" {
 
@@ -2689,6 +2689,7 @@ static void conv_x3_params(ConvParams& p, const float* x0, int c0, const float* 
   conv_params(p, x0, c0, x1, c1, N, H, (const float*)wx3, bias, cin_pad, cout, cout, 64, 9, res, out);
   p.opt_bm128 = 0;
   p.x3_nprod = 3;
+  p.opt_img8_partial = 1;  // four-image 8 x 8 tiles at any N (every tile-origin-derived read stays in the batch)
   if (taps == 1) {  // (two sources: the output blocks' concat, read by channel range)
     p.s0 = x0; p.sc0 = c0; p.s1 = c1 ? x1 : nullptr; p.sc1 = c1;
     p.wskip = (const float*)wx3; p.cs_pad = cin_pad;

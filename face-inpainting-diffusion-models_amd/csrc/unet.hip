@@ -832,7 +832,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
         prof_begin(s, &pe, "act_pool");
         const int e = launch_act_apply(in0, c0, N, H * H, act, A, Bc, ws_ + ly_.o_pool_, s);
         prof_end(s, pe, "act_pool", 0.0, 8.0 * N * (double)H * H * c0);
-        IFD_REQUIRE(e == 0, "act_apply launch");
+        IFD_LAUNCH_OK(e, "act_apply");
       }
       p = q;
       act = ACT_NONE;
@@ -873,7 +873,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
       if (!e && pool_res && res != pooled_prev)
         e = launch_act_pool(res, cw.cout, N, resH, ACT_NONE, nullptr, nullptr, ws_ + ly_.o_pool2_, nullptr, s);
       prof_end(s, pe, "act_pool", 0.0, 4.0 * N * (double)Hin * Hin * (c0 + (pool_res ? cw.cout : 0)) * 1.25);
-      IFD_REQUIRE(e == 0, "act_pool launch");
+      IFD_LAUNCH_OK(e, "act_pool");
       p = q;
       if (pool_in) {
         xf = XF_NONE;
@@ -1002,7 +1002,7 @@ int Model::run_conv(const ConvW& cw, const float* in0, int c0, const float* in1,
   }
   if (prof_on_ && e0) prof_end(s, e0, nm, flops, bytes);
   if (e) {
-    set_error(std::string("conv launch failed: ") + hipGetErrorString((hipError_t)e));
+    set_error(std::string("conv launch failed (") + nm + "): " + hipGetErrorString((hipError_t)e));
     return 1;
   }
   return 0;
@@ -1054,14 +1054,14 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
   (void)part;
   int e = run_gn(in0, c0, in1, c1, N, Hin * Hin, r.gn1, nullptr, 0, 0, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, Hin * Hin, c0 + c1));
-  IFD_REQUIRE(e == 0, "gn launch");
+  IFD_LAUNCH_OK(e, "gn");
   if (run_conv(r.conv1, in0, c0, in1, c1, N, Hin, H, r.xf, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
                0, t1, EPI_NHWC, s))
     return 1;
   prof_begin(s, &g0, "groupnorm_stats");
   e = run_gn(t1, r.cout, nullptr, 0, N, H * H, r.gn2, ws_ + ly_.o_E_, emb_total_, r.emb_off, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, H * H, r.cout));
-  IFD_REQUIRE(e == 0, "gn launch");
+  IFD_LAUNCH_OK(e, "gn");
   // split modes: skip_connection(x) as its own launch into `out`, then conv2 adds it as its residual
   // in place (each output element's residual is read by the thread that writes it)
   const bool split_mode = prec_ == IFD_PREC_3XF16 || prec_ == IFD_PREC_F16;
@@ -1091,7 +1091,7 @@ int Model::run_res(const ResP& r, const float* in0, int c0, const float* in1, in
       const int e2 = launch_skip_x3(q, s);
       if (prof_on_ && e0) prof_end(s, e0, nm, 2.0 * pix * r.cout * (c0 + q.sc1), 4.0 * pix * (c0 + q.sc1 + r.cout));
       if (e2) {
-        set_error(std::string("skip launch failed: ") + hipGetErrorString((hipError_t)e2));
+        set_error(std::string("skip launch failed (") + nm + "): " + hipGetErrorString((hipError_t)e2));
         return 1;
       }
       return run_conv(r.conv2_res, t1, r.cout, nullptr, 0, N, H, H, XF_NONE, ACT_AFFINE_SILU, A, Bc, nullptr, 0,
@@ -1113,7 +1113,7 @@ int Model::run_attn(const AttnP& a, const float* in, int N, int Hin, float* out,
   prof_begin(s, &g0, "groupnorm_stats");
   int e = run_gn(in, a.C, nullptr, 0, N, T, a.gn, nullptr, 0, 0, A, Bc, s);
   prof_end(s, g0, "groupnorm_stats", 0.0, gn_bytes(N, T, a.C));
-  IFD_REQUIRE(e == 0, "gn launch");
+  IFD_LAUNCH_OK(e, "gn");
   if (run_conv(a.qkv, in, a.C, nullptr, 0, N, Hin, Hin, XF_NONE, ACT_AFFINE, A, Bc, nullptr, 0, nullptr, 0, nullptr, 0,
                0, qkv, EPI_NHWC, s))
     return 1;
@@ -1223,7 +1223,7 @@ int Model::forward(const float* x, const float* a, const float* m, int pack_mode
   prof_begin(s, &p0, "groupnorm_stats");
   int e = run_gn(cur, cur_c, nullptr, 0, B, R * R, gn_out_, nullptr, 0, 0, A, Bc, s);
   prof_end(s, p0, "groupnorm_stats", 0.0, gn_bytes(B, R * R, cur_c));
-  IFD_REQUIRE(e == 0, "gn launch");
+  IFD_LAUNCH_OK(e, "gn");
   return run_conv(conv_out_, cur, cur_c, nullptr, 0, B, R, R, XF_NONE, ACT_AFFINE_SILU, A, Bc, nullptr, 0, nullptr, 0,
                   nullptr, 0, 0, out6, epi, s, sc, img, gt, mask, noise, known);
 }

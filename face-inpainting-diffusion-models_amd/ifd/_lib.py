@@ -50,6 +50,7 @@ EXPORTS = {
     "ifd_create": (ctypes.c_int, [ctypes.POINTER(IfdConfig), ctypes.POINTER(ctypes.c_void_p)]),
     "ifd_destroy": (None, [ctypes.c_void_p]),
     "ifd_last_error": (ctypes.c_char_p, []),
+    "ifd_clear_error": (None, []),
     "ifd_version": (ctypes.c_char_p, []),
     "ifd_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ifd_profile_report": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]),
@@ -123,9 +124,14 @@ def lib():
 
 
 def check(rc):
+    """Raise on a non-zero status with the message the failing entry point set (include/ifd.h: every non-zero
+    status sets one naming its entry). The message is cleared once read, so it is never reported again for a
+    later call's status."""
     if rc != 0:
-        msg = lib().ifd_last_error()
-        raise RuntimeError(f"ifd: {msg.decode() if msg else 'error'} (status {rc})")
+        L = lib()
+        msg = L.ifd_last_error()
+        L.ifd_clear_error()
+        raise RuntimeError(f"ifd: {msg.decode() if msg else 'error (no message set)'} (status {rc})")
 
 
 def ptr(t):

@@ -60,6 +60,9 @@ typedef struct ifd_handle ifd_handle;
 int ifd_create(const ifd_config* cfg, ifd_handle** out);
 void ifd_destroy(ifd_handle* h);
 const char* ifd_last_error(void);
+/* Clears the thread-local message (ifd._lib.check does after reporting one, so a message is never reported
+ * for a later status). Every non-zero status sets its own message naming the entry point that returned it. */
+void ifd_clear_error(void);
 
 /* Parameter inventory of the model (state_dict order, names without "base_model."). No GPU use. */
 int ifd_num_params(ifd_handle* h, int* n);

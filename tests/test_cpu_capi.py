@@ -116,3 +116,35 @@ def test_workspace_plan_is_activation_bound():
     wb, ws = ctypes.c_int64(), ctypes.c_int64()
     assert L.ifd_memory(h.h, ctypes.byref(wb), ctypes.byref(ws)) == 0 and ws.value == 0
     assert L.ifd_workspace_plan(h.h, 0, ctypes.byref(ws)) != 0
+
+
+def test_every_launch_status_sets_its_message():
+    """Error contract (SURVEY §8(b) "Errors"): no entry point hands back a raw hipGetLastError() status without
+    setting a message for it; hipGetLastError is read only by ifd::launch_status (csrc/common.h), which names the
+    function it is called from."""
+    csrc = os.path.join(ROOT, "face-inpainting-diffusion-models_amd", "csrc")
+    offenders = []
+    for fn in sorted(os.listdir(csrc)):
+        if not fn.endswith((".hip", ".h")):
+            continue
+        for i, line in enumerate(open(os.path.join(csrc, fn)), 1):
+            if "hipGetLastError" in line and not line.lstrip().startswith("//"):
+                offenders.append(f"{fn}:{i}: {line.strip()}")
+    assert offenders == ["common.h:20: const hipError_t e = hipGetLastError();"], offenders
+    tr = open(os.path.join(csrc, "train_ops.hip")).read()
+    assert "#define TR_LAST() IFD_LAUNCH_STATUS()" in tr
+
+
+def test_check_reports_then_clears_the_message():
+    """_lib.check raises with the failing entry's message and clears it, so a later status is never reported
+    with this call's message (the round-5 stale 'shape not eligible' message of a status-700 fault)."""
+    from ifd import _lib
+    L = _lib.lib()
+    rc = L.ifd_workspace_plan(None, 1, None)
+    assert rc != 0
+    with pytest.raises(RuntimeError, match="ifd_workspace_plan"):
+        _lib.check(rc)
+    assert L.ifd_last_error() == b""
+    rc = L.ifd_tr_scale(None, 4, 1.0, None)
+    with pytest.raises(RuntimeError, match="ifd_tr_scale: bad arguments"):
+        _lib.check(rc)
