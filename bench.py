@@ -203,55 +203,63 @@ def spawn_ranks(n):
     return subprocess.run(cmd, env=env).returncode
 
 
-def train_main(args):
-    """`--workload train`: BASELINE configs[4]'s training step (code/train_inpainting.py:15-79), B images per GPU
-    at 256x256: t ~ randint, training_losses with injection, backward, clip_grad_norm_(1.0), AdamW. Step = one
-    optimizer step. --precision 3xf16 (default): forward, dgrad and wgrad 3x3 convs on the fp32-accurate
-    split kernels (ifd/train.py UNetTrainer precision="3xf16"); fp32: every conv on fp32 MFMA, as the reference
-    trains (no bf16 / LoRA exists in the reference). At N=1 the other mode is timed beside it.
-    Multi-GPU: per-rank steps (data parallelism would add an all-reduce of the 374 MB gradient; not part of
-    the reference, which trains on one device)."""
+def time_train(dev, B, precision, steps, warmup, rank=0):
+    """`steps` timed training steps (after `warmup` untimed ones) of BASELINE configs[4] on `dev`: B synthetic 256x256
+    images, t ~ randint, training_losses with injection, backward, clip_grad_norm_(1.0), AdamW
+    (code/train_inpainting.py:15-79). Returns (max-over-ranks seconds, last loss, guard trips)."""
     from ifd import parallel
     from ifd.manifest import make_state_dict
     from ifd.schedules import create_gaussian_diffusion
-    from ifd.topology import FULL, gflop_per_image
+    from ifd.topology import FULL
     from ifd.train import UNetTrainer
+    H = FULL.image_size
+    diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="quadratic")
+    gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
+    masked = gt * (1 - mask)
+    tr = UNetTrainer(FULL, device=dev, precision=precision, fuse_gn=os.environ.get("IFD_TRAIN_FUSE_GN", "1") != "0",
+                     fuse_gnb=os.environ.get("IFD_TRAIN_FUSE_GNB", "1") != "0")
+    tr.load_state_dict(make_state_dict(FULL, seed=1))
+    gen = torch.Generator(device=dev).manual_seed(1 + rank)
+
+    def step():
+        t = torch.randint(0, 1000, (B,), device=dev, generator=gen)
+        return tr.train_step(diff, gt, masked, mask, t)
+    for _ in range(warmup):
+        step()
+    parallel.barrier(dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    parallel.barrier(dev)
+    el = parallel.max_over_ranks(time.perf_counter() - t0, dev)
+    lv = float(loss)
+    assert math.isfinite(lv)
+    trips = tr.guard_trips
+    del tr
+    torch.cuda.empty_cache()
+    return el, lv, trips
+
+
+def train_main(args):
+    """`--workload train`: BASELINE configs[4]'s training step (code/train_inpainting.py:15-79), B images per GPU
+    at 256x256 (time_train). Step = one optimizer step. --precision 3xf16 (default): forward, dgrad and wgrad 3x3
+    convs on the fp32-accurate split kernels (ifd/train.py UNetTrainer precision="3xf16"); fp32: every conv on fp32
+    MFMA, as the reference trains (no bf16 / LoRA exists in the reference). At N=1 the other mode is timed beside it.
+    Multi-GPU: per-rank steps (data parallelism would add an all-reduce of the 374 MB gradient; not part of
+    the reference, which trains on one device)."""
+    from ifd import parallel
+    from ifd.topology import FULL, gflop_per_image
     rank, ws, local = parallel.world()
     dev = parallel.device_for(local)
     torch.cuda.set_device(dev)
     parallel.init(device=dev)
-    B, H = args.batch, FULL.image_size
+    B = args.batch
     prec = args.precision
-    diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="quadratic")
-    gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
-    masked = gt * (1 - mask)
-    sd = make_state_dict(FULL, seed=1)
 
     def run(precision, steps, warmup):
-        tr = UNetTrainer(FULL, device=dev, precision=precision, fuse_gn=os.environ.get("IFD_TRAIN_FUSE_GN", "1") != "0",
-                         fuse_gnb=os.environ.get("IFD_TRAIN_FUSE_GNB", "1") != "0")
-        tr.load_state_dict(sd)
-        gen = torch.Generator(device=dev).manual_seed(1 + rank)
-
-        def step():
-            t = torch.randint(0, 1000, (B,), device=dev, generator=gen)
-            return tr.train_step(diff, gt, masked, mask, t)
-        for _ in range(warmup):
-            step()
-        parallel.barrier(dev)
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            loss = step()
-        torch.cuda.synchronize(dev)
-        parallel.barrier(dev)
-        el = parallel.max_over_ranks(time.perf_counter() - t0, dev)
-        lv = float(loss)
-        assert math.isfinite(lv)
-        trips = tr.guard_trips
-        del tr
-        torch.cuda.empty_cache()
-        return el, lv, trips
+        return time_train(dev, B, precision, steps, warmup, rank)
 
     elapsed, lossv, trips = run(prec, args.steps, args.warmup)
     value = B * ws * args.steps / elapsed
@@ -400,6 +408,10 @@ def build_parser():
     ap.add_argument("--f16-steps", type=int, default=1,
                     help="N=1 only: also time this many steps in the reduced-precision f16 mode, reported separately "
                          "(the reference's .half() experiment, code/test_quant.py:390-409; 0 = skip)")
+    ap.add_argument("--train-steps", type=int, default=5,
+                    help="sample workload, N=1 only: also time this many 3xf16 training steps (BASELINE configs[4], "
+                         "B=--train-batch, after one warm-up step), reported as `train` beside the headline (0 = skip)")
+    ap.add_argument("--train-batch", type=int, default=32, help="images per training step of the `train` leg")
     ap.add_argument("--ddpm-steps", type=int, default=1000, help="--workload ddpm: diffusion steps T (linear)")
     ap.add_argument("--workload", choices=["sample", "c4", "train", "ddpm", "dropin"], default="sample",
                     help="sample: the headline DDIM-100 sampler, --batch images per GPU (default; configs[1]); c4: the "
@@ -574,7 +586,7 @@ def main():
                                 "T=1000 eta=0.75, all_gather of the outputs (BASELINE configs[3])" if c4 else
                                 "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1]) "
                                 "through the reference script's per-step loop over model() "
-                                "(code/test_inp_ddim_100.py:470-576, lazy range guard)" if dropin else
+                                "(code/test_inp_ddim_100.py:470-576, sync range guard)" if dropin else
                                 "256x256 9-ch UNet inpainting, DDIM-100 cosine T=1000 eta=0.75 (BASELINE configs[1])"),
                    "options": opts,
                    "global_batch": G, "batch_per_gpu": B if G % ws == 0 else f"{G // ws}-{-(-G // ws)}",
@@ -626,6 +638,21 @@ def main():
                               "ms_per_step": round(el16 / args.f16_steps * 1e3, 2), "steps": args.f16_steps,
                               "warmup": 1, "dtype": "f16 operands, fp32 accumulate (not fp32-class; "
                                                     "tests/test_gpu_f16.py records its error)"}
+    if extras and args.train_steps > 0:
+        # BASELINE configs[4] on the driver's clock: the 3xf16 training step at B = 32 (time_train), after the
+        # sampler's lines; the sampler's workspace arena is released first
+        model._handle = model._lz = None
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        elt, lt, tt = time_train(dev, args.train_batch, "3xf16", args.train_steps, 1)
+        res["train"] = {"value": round(args.train_batch * args.train_steps / elt, 4), "unit": "images/s",
+                        "ms_per_step": round(elt / args.train_steps * 1e3, 2), "steps": args.train_steps, "warmup": 1,
+                        "batch": args.train_batch, "loss": lt, "guard_trips": tt,
+                        "workload": "train_inpainting.py train_epoch step: training_losses + backward + "
+                                    "clip_grad_norm_(1.0) + AdamW, 256x256 9-ch UNet (BASELINE configs[4])",
+                        "dtype": "f32 (3xf16 split MFMA for the forward, dgrad and wgrad convs)",
+                        "algorithmic_tflops": round(3 * gflop_per_image(FULL) * args.train_batch * args.train_steps
+                                                    / elt / 1e3, 2)}
     if rank == 0 and kernels:
         res["kernels"] = {k: {"count": int(v["count"]), "ms": round(v["ms"], 3)} for k, v in kernels.items()}
     # the process group goes first: no rank then waits inside a collective while rank 0 times the CPU path

@@ -12,14 +12,16 @@ There is no CPU/PyTorch fallback: a CPU tensor or a missing library raises.
 
 precision="3xf16" is guarded: the split kernels flag any operand that reaches the f16 range
 (include/ifd.h ifd_guard_*). Two ways to act on the flag (`guard=`, env IFD_GUARD):
-* "lazy" (the default): a forward never waits on the GPU. Each 3xf16 forward enqueues an asynchronous
-  copy of the (sticky) guard word into page-locked memory; the next forwards look at the copies whose
-  work has finished. A trip raises RuntimeError from a LATER forward (or from `guard_check()`), at most
-  a few forwards after the one that tripped; the outputs of the forwards in between are not recomputed —
-  the caller re-runs its loop, e.g. with precision="fp32". This is what a reference script's own loop
-  (model() once per step, code/test_inp_ddim_100.py:512-574) runs into, at no per-step cost.
-* "sync": each forward checks the guard after its launch (one stream synchronisation) and recomputes a
-  flagged forward in exact fp32 (counted in `guard_trips`): fp32-class for any input.
+* "sync" (the default since round 6): each forward checks the guard after its launch (one stream
+  synchronisation) and recomputes a flagged forward in exact fp32 (counted in `guard_trips`) before
+  returning it: fp32-class for any input, so an unchanged reference script's own loop (model() once per
+  step, code/test_inp_ddim_100.py:512-574) survives a trip with the fp32 run's result. Measured cost on
+  that loop: none (8.733 vs 8.716 images/s with "lazy", the same box, profiles/r06a/bench_dropin_*.json):
+  the GPU work of one forward (~18 ms at B = 16) dwarfs the host's enqueue of the next.
+* "lazy": a forward never waits on the GPU. Each 3xf16 forward enqueues an asynchronous copy of the
+  (sticky) guard word into page-locked memory; the next forwards look at the copies whose work has
+  finished. A trip raises RuntimeError from a LATER forward (or from `guard_check()`), at most a few
+  forwards after the one that tripped; the outputs of the forwards in between are not recomputed.
 The fused sampler loops (ifd.sampler) check once per loop and re-run the whole loop in fp32, in both.
 """
 from __future__ import annotations
@@ -91,7 +93,7 @@ class DiffusionInpaintingModel(torch.nn.Module):
     def __init__(self, cfg: UNetConfig = FULL, device=None, precision: str = "3xf16", options=None, guard=None):
         super().__init__()
         self.cfg = cfg
-        self.guard = guard or os.environ.get("IFD_GUARD", "lazy")  # module docstring
+        self.guard = guard or os.environ.get("IFD_GUARD", "sync")  # module docstring
         if self.guard not in ("lazy", "sync"):
             raise ValueError("guard must be 'lazy' or 'sync'")
         # handle options (include/ifd.h ifd_set_option), e.g. {"batch_invariant": 1}
@@ -117,7 +119,7 @@ class DiffusionInpaintingModel(torch.nn.Module):
         self.guard_trips = 0  # 3xf16 evals / loops recomputed in fp32 by the range guard
         self._applied = None  # (handle, precision, options) last pushed to the library
         self._deferred = None  # deferred_guard(): per-forward guard reads suspended
-        self._lz = None  # lazy guard: [handle id, pinned slots, pending [(event, slot)], next slot, armed]
+        self._lz = None  # lazy guard: [handle, pinned slots, pending [(event, slot)], next slot, armed]
 
     # -- weights -------------------------------------------------------------------------------
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
@@ -199,8 +201,10 @@ class DiffusionInpaintingModel(torch.nn.Module):
     def _lazy_forward(self, h, dev, launch):
         L = _lib.lib()
         s = _lib.stream_ptr(dev)
-        if self._lz is None or self._lz[0] != id(h):
-            self._lz = [id(h), torch.zeros(self._LZ_SLOTS, dtype=torch.int32, pin_memory=True), [], 0, False]
+        if self._lz is None or self._lz[0] is not h:
+            if self._lz is not None:
+                self.guard_check()  # the old handle's copies still pending are read (a trip there is reported)
+            self._lz = [h, torch.zeros(self._LZ_SLOTS, dtype=torch.int32, pin_memory=True), [], 0, False]
         lz = self._lz
         self._lazy_poll(block=len(lz[2]) >= self._LZ_SLOTS)  # a full ring waits for its oldest copy
         if not lz[4]:  # armed once: the word is sticky, so one reset covers every later forward

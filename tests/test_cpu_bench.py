@@ -109,3 +109,13 @@ def test_fp32_accuracy_note_reads_newest_parity(tmp_path, monkeypatch):
     assert note["per_eval_error_vs_reference_own"] == {"mean": 2.0, "p999": 2.0, "max": 2.0}
     assert note["source"].endswith("r02x/parity.json")
     assert "NOT fp32-class" in note["note"]
+
+
+def test_headline_line_carries_a_training_leg():
+    """BASELINE configs[4] on the driver's clock: the default N=1 bench run times 3xf16 training steps at B = 32
+    (`train` in the JSON line) after the sampler's lines; the profiler passes of tools/gpu_round.sh switch it off."""
+    import bench
+    a = bench.build_parser().parse_args([])
+    assert a.train_steps == 5 and a.train_batch == 32
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "gpu_round.sh")).read()
+    assert src.count("--train-steps 0") == 2

@@ -131,6 +131,7 @@ def _reduced_steps(precision, B, steps):
     img = torch.rand(B, 3, 64, 64, generator=g) * 2 - 1
     mask = (torch.rand(B, 1, 64, 64, generator=g) > 0.5).float()
     t = torch.randint(0, 1000, (B,), generator=g)
+    torch.manual_seed(5)  # the steps' noise draws (noise_device="cpu": the global CPU generator)
     losses = []
     for _ in range(steps):  # asynchronous: no synchronisation between the steps (the round-5 repro)
         losses.append(tr.train_step(diff, img.to(DEV), (img * (1 - mask)).to(DEV), mask.to(DEV), t.to(DEV),

@@ -243,13 +243,13 @@ def test_x3_range_guard_forward(evals, record):
 
 
 def test_x3_range_guard_lazy(evals):
-    """guard="lazy" (the default): forwards never wait on the GPU; a trip is reported by a later forward
+    """guard="lazy" (opt-in since round 6): forwards never wait on the GPU; a trip is reported by a later forward
     or by guard_check() as a RuntimeError (the flagged outputs are not recomputed), counted once, and the
     guard is re-armed afterwards: in-range forwards of the same model then pass again."""
     from ifd.model import DiffusionInpaintingModel
     x, gt, mask = (_t(evals[f"full/{k}"]).to(DEV) for k in ("x", "gt", "mask"))
     t = torch.tensor([500], device=DEV)
-    m3 = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16")
+    m3 = DiffusionInpaintingModel(FULL, device=DEV, precision="3xf16", guard="lazy")
     assert m3.guard == "lazy"
     m3.load_state_dict(_scaled_state_dict())
     with torch.no_grad():
@@ -265,6 +265,33 @@ def test_x3_range_guard_lazy(evals):
             m3(x, t, masked_image=gt * (1 - mask), mask=mask)
         m3.guard_check()
     assert m3.guard_trips == 1
+
+
+def test_x3_range_guard_dropin_script_loop(record):
+    """The drop-in default survives a trip: the UNCHANGED reference script loop (bench.script_ddim_pass restates
+    code/test_inp_ddim_100.py:470-576: model() once per step, the DDIM update and injection in torch) over a 3xf16
+    model whose layer trips the guard at every forward completes, and its output equals the fp32 model's run of
+    the same loop bit for bit (the default guard="sync" recomputes each flagged forward in fp32 before returning
+    it)."""
+    from bench import script_ddim_pass, synth_inputs
+    from ifd.model import DiffusionInpaintingModel
+    from ifd.schedules import create_gaussian_diffusion
+    sd = _scaled_state_dict()
+    diff = create_gaussian_diffusion(steps=1000, learn_sigma=True, noise_schedule="cosine")
+    gt, mask = synth_inputs(2, 256, seed=7, device=DEV)
+    outs = {}
+    for prec in ("3xf16", "fp32"):
+        m = DiffusionInpaintingModel(FULL, device=DEV, precision=prec)
+        m.load_state_dict(sd)
+        torch.manual_seed(4)
+        with torch.no_grad(), (pytest.warns(UserWarning, match="range guard") if prec == "3xf16"
+                               else __import__("contextlib").nullcontext()):
+            outs[prec] = script_ddim_pass(m, diff.alphas_cumprod, (2, 3, 256, 256), gt, mask, 5, 0.75, DEV)
+        if prec == "3xf16":
+            assert m.guard == "sync" and m.guard_trips == 6  # every forward of the 6-step loop (999 .. 0)
+    record("x3_range_guard/dropin_script_loop", maxabs_vs_fp32=maxabs(outs["3xf16"], outs["fp32"]))
+    assert torch.isfinite(outs["3xf16"]).all()
+    assert torch.equal(outs["3xf16"], outs["fp32"])
 
 
 def test_x3_range_guard_quiet_on_manifest(evals, x3_model):

@@ -12,9 +12,9 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 500 python $R/bench.py --steps $STEPS --warmup 1 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { echo "bench failed rc=$?"; exit 1; }
 echo "bench ok"; tail -c 600 $OUT/bench_$TAG.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o trace --output-format csv -- \
-   python $R/bench.py --steps 1 --warmup 1 --cpu-baseline-seconds 0 --fp32-exact-steps 0 > $OUT/prof_$TAG.log 2>&1 || { echo "rocprof trace failed rc=$?"; exit 1; }
+   python $R/bench.py --steps 1 --warmup 1 --cpu-baseline-seconds 0 --fp32-exact-steps 0 --train-steps 0 > $OUT/prof_$TAG.log 2>&1 || { echo "rocprof trace failed rc=$?"; exit 1; }
 echo "trace ok"
-BARGS="--steps 1 --warmup 0 --ddim-steps 10 --no-profile --cpu-baseline-seconds 0 --fp32-exact-steps 0"
+BARGS="--steps 1 --warmup 0 --ddim-steps 10 --no-profile --cpu-baseline-seconds 0 --fp32-exact-steps 0 --f16-steps 0 --train-steps 0"
 i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
