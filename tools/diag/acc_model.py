@@ -9,7 +9,8 @@ Every conv of the oracle UNet is replaced by an emulation of how the MFMA kernel
   * x3wino:    Winograd F(2x2,3x3) for the 3x3 convs (round 6): the input transform B^T d B in fp32
                (adds only, as a producer wave would stage it), the weight transform G g G^T in fp64 then split
                like the weights above, the 16 elementwise GEMMs over K = Cin on the x3sep arithmetic, the output
-               transform A^T M A in fp32 (1x1 convs stay x3sep);
+               transform A^T M A in fp32 (1x1 convs stay x3sep); x3wino1: the same with the correction products
+               in the main accumulator (no second accumulator set: half the registers);
   * ref:       torch's fp32 conv (the reference's arithmetic class).
 and compared against the fp64 UNet. Usage: python tools/diag/acc_model.py [reduced|full] [t]
 """
@@ -37,7 +38,7 @@ _G = torch.tensor([[1, 0, 0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0, 0, 1]], dty
 _AT = torch.tensor([[1, 1, 1, 0], [0, 1, -1, -1]], dtype=torch.float64)
 
 
-def wino_emul(x, w, b):
+def wino_emul(x, w, b, sep=True):
     """F(2x2,3x3), padding 1, even H and W: Y = A^T [ (G g G^T) . (B^T d B) ] A per 2x2 output tile."""
     n, c, _, _ = w.shape
     B, _, H, W = x.shape
@@ -62,7 +63,7 @@ def wino_emul(x, w, b):
             for g in range(2):
                 cs = slice(c0 + 8 * g, c0 + 8 * g + 8)
                 s = torch.einsum("xnk,bkxt->bnxt", ua[:, :, cs], va[:, cs].double())
-                if lo:
+                if lo and sep:
                     accl = (accl.double() + s).float()
                 else:
                     acc = (acc.double() + s).float()
@@ -77,9 +78,9 @@ def wino_emul(x, w, b):
 def conv_emul(mode, x, w, b, padding=0):
     if mode == "ref":
         return F.conv2d(x, w, b, padding=padding)
-    if mode == "x3wino":
+    if mode in ("x3wino", "x3wino1"):
         if w.shape[-1] == 3 and padding == 1 and x.shape[-1] % 2 == 0 and x.shape[-2] % 2 == 0:
-            return wino_emul(x, w, b)
+            return wino_emul(x, w, b, sep=mode == "x3wino")
         mode = "x3sep"
     n, c, kh, kw = w.shape
     T = kh * kw
