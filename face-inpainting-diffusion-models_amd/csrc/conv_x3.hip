@@ -796,6 +796,27 @@ __device__ __forceinline__ void conv_x3_body(const ConvParams& p, const GnbParam
     // and the epilogue adds over the wave's 64 pixels, per channel, A1 = sum dz, A2 = sum dz nrm and
     // A3 = (1 + s) sum dz xhat - gn_bwd_partial_kernel's pass 1 (train_ops.hip) without its pass over (da, x).
     // The outputs are then stored as in the other epilogues (deferred from xr, or at once from acc).
+    // GNB: the epilogue's per-(image, channel) parameters (mean, rstd, gamma, beta, 1 + scale, shift) of both channel
+    // blocks, all twelve loads issued together at the epilogue's start (round 5 loaded nr = 1's after nr = 0's sums:
+    // two rounds of global-load latency between every unit's MFMAs and its successor's). Loaded earlier, during the
+    // unit's last chunks beside the prefetched x, they spilled 33-98 VGPRs (round 6, -Rpass-analysis)
+    float gpf[GNB ? 2 : 1][6];
+    auto gnb_params = [&](const STile& t) __attribute__((always_inline)) {
+      if constexpr (GNB) {
+        const int ll = lane_id() & 31;
+        const int n = t.n0 + wimg, C = p.cout, cpg = C / 32;
+#pragma unroll
+        for (int nr = 0; nr < 2; ++nr) {
+          const int cc = t.ct * XBN + 32 * nr + ll, grp = cc / cpg;
+          gpf[nr][0] = g.stats[(n * 32 + grp) * 2];
+          gpf[nr][1] = g.stats[(n * 32 + grp) * 2 + 1];
+          gpf[nr][2] = g.gamma[cc];
+          gpf[nr][3] = g.beta[cc];
+          gpf[nr][4] = g.ss ? 1.0f + g.ss[(size_t)n * g.ss_stride + cc] : 1.0f;
+          gpf[nr][5] = g.ss ? g.ss[(size_t)n * g.ss_stride + C + cc] : 0.0f;
+        }
+      }
+    };
     auto epilogue_gnb = [&](const STile& t, float (&xv)[2][2][16], bool dfr) {
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr)
@@ -807,15 +828,14 @@ __device__ __forceinline__ void conv_x3_body(const ConvParams& p, const GnbParam
             acc[mr][nr][r] = x + bias2[nr];
           }
       const int ln = lane_id(), ll = ln & 31;
-      const int n = t.n0 + wimg, C = p.cout, cpg = C / 32;
+      const int n = t.n0 + wimg, C = p.cout;
       float a1[2], a2[2], a3[2], onep[2];
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr) {
-        const int cc = t.ct * XBN + 32 * nr + ll, grp = cc / cpg;
-        const float mean = g.stats[(n * 32 + grp) * 2], rstd = g.stats[(n * 32 + grp) * 2 + 1];
-        const float gam = g.gamma[cc], bet = g.beta[cc];
-        onep[nr] = g.ss ? 1.0f + g.ss[(size_t)n * g.ss_stride + cc] : 1.0f;
-        const float sh = g.ss ? g.ss[(size_t)n * g.ss_stride + C + cc] : 0.0f;
+        // the per-(image, channel) GroupNorm parameters, loaded during the unit's last chunks (gnb_params)
+        const float mean = gpf[nr][0], rstd = gpf[nr][1], gam = gpf[nr][2], bet = gpf[nr][3];
+        onep[nr] = gpf[nr][4];
+        const float sh = gpf[nr][5];
         float s1 = 0.f, s2 = 0.f, s3 = 0.f;
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1162,6 +1182,7 @@ __device__ __forceinline__ void conv_x3_body(const ConvParams& p, const GnbParam
                        (nmain - 2 >= X3_DEFER || (!X3_DEFER1_OFF && nmain == 1 && !p.res && !gnbu));
       if constexpr (GNB) {  // (launched only with gnb_part set and S == 1)
         (void)gnbu;
+        gnb_params(t);
         epilogue_gnb(t, xr, dfr);
       } else {
         if (dfr)

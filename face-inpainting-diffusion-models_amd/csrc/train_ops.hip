@@ -896,6 +896,11 @@ constexpr int WS_NTP = 256;                                  // producer threads
                   // 2 consumers without MFMAs, 3 no range-guard max, 4 the split without the lo part, 5 no LDS
                   // writes, 6 no split / max (raw bits written), 7 no global loads after the first chunk
 #endif
+#ifndef WS_WC
+// widest chunk row of the 64-pixel chunks: 8 x 8 pixels (X halo 10 x 10 = 100 pixels to stage and activate) since
+// round 6; 2 x 32 (halo 4 x 34 = 136) before: 240.4 vs 236.9 training images/s, 4 x 16 239.1 (profiles/r06c)
+#define WS_WC 8
+#endif
 #define WS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 #if WS_ABL == 2
 #define WS_MFMA(a, b, c, x, y, z) ([&]() { asm volatile("" ::"v"(a), "v"(b)); return (c); }())
@@ -905,7 +910,11 @@ constexpr int WS_NTP = 256;                                  // producer threads
 template <int NPROD, bool GNA>
 __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* guard, float* colpart) {
   constexpr int DI = WX_PX * 16 / WS_NTP;                    // dY 16-B items per producer thread (4)
-  constexpr int XI = (WX_HMAX * 16 + WS_NTP - 1) / WS_NTP;   // X halo items per producer thread (9)
+  // X halo items per producer thread: the largest halo of a chunk shape the kernel can take (a map narrower than
+  // WS_WC takes its own width): 8 x 8 chunks 100 pixels (7 items), 4 x 16 108 (7), 2 x 32 136 (9)
+  constexpr int HPMAX = WS_WC >= 32 ? 136 : (WS_WC >= 16 ? 108 : 100);
+  static_assert(HPMAX <= WX_HMAX, "halo fits the stage");
+  constexpr int XI = (HPMAX * 16 + WS_NTP - 1) / WS_NTP;
   constexpr int NTAP = 9;
   __shared__ __attribute__((aligned(16))) _Float16 lds[2][WX_D + WX_X];
   f32x4* const csred = reinterpret_cast<f32x4*>(&lds[0][0]);  // after the chunk loop
@@ -925,7 +934,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_ws_kernel(WgArgs a, unsigned* gu
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool producer = wave >= 4;
-  const int Wc = a.W < 32 ? a.W : 32, R = WX_PX / Wc;
+  const int Wc = a.W < WS_WC ? a.W : WS_WC, R = WX_PX / Wc;
   const int HWc = Wc + 2, HP = (R + 2) * HWc;
   const int lwc = __builtin_ctz(Wc);
   const int segs = a.W / Wc, rows_per_img = a.H / R;
