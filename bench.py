@@ -644,7 +644,14 @@ def main():
         model._handle = model._lz = None
         torch.cuda.synchronize(dev)
         torch.cuda.empty_cache()
-        elt, lt, tt = time_train(dev, args.train_batch, "3xf16", args.train_steps, 1)
+        try:
+            elt, lt, tt = time_train(dev, args.train_batch, "3xf16", args.train_steps, 1)
+        except Exception as e:  # the headline line is still printed; the failure is reported in it
+            print(f"bench: training leg failed: {e!r}", file=sys.stderr)
+            elt = None
+    if extras and args.train_steps > 0 and elt is None:
+        res["train"] = {"error": "the training leg raised (stderr has the exception)"}
+    elif extras and args.train_steps > 0:
         res["train"] = {"value": round(args.train_batch * args.train_steps / elt, 4), "unit": "images/s",
                         "ms_per_step": round(elt / args.train_steps * 1e3, 2), "steps": args.train_steps, "warmup": 1,
                         "batch": args.train_batch, "loss": lt, "guard_trips": tt,
