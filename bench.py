@@ -217,7 +217,8 @@ def time_train(dev, B, precision, steps, warmup, rank=0):
     gt, mask = synth_inputs(B, H, seed=7 + rank, device=dev)
     masked = gt * (1 - mask)
     tr = UNetTrainer(FULL, device=dev, precision=precision, fuse_gn=os.environ.get("IFD_TRAIN_FUSE_GN", "1") != "0",
-                     fuse_gnb=os.environ.get("IFD_TRAIN_FUSE_GNB", "1") != "0")
+                     fuse_gnb=os.environ.get("IFD_TRAIN_FUSE_GNB", "1") != "0",
+                     gnb_act=os.environ.get("IFD_TRAIN_GNB_ACT", "0") != "0")
     tr.load_state_dict(make_state_dict(FULL, seed=1))
     gen = torch.Generator(device=dev).manual_seed(1 + rank)
 

@@ -109,6 +109,7 @@ struct GnbParams {
   const float* ss; int ss_stride;  // optional scale [n][c], shift [n][cout + c]
   int silu;
   float* part; int nsl;
+  float* act;  // optional: the GroupNorm's forward output silu(z) (or z), [N][H][W][cout] (the next weight gradient's input)
 };
 int launch_conv_x3_gnb(const ConvParams& p, const GnbParams& g, hipStream_t stream);
 

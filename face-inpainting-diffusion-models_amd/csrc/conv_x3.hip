@@ -830,6 +830,12 @@ __device__ __forceinline__ void conv_x3_body(const ConvParams& p, const GnbParam
       const int ln = lane_id(), ll = ln & 31;
       const int n = t.n0 + wimg, C = p.cout;
       float a1[2], a2[2], a3[2], onep[2];
+      // g.act: the GroupNorm's forward output act = silu(z) (or z), the input of the conv whose weight gradient
+      // follows, written at the dgrad output's addresses (same [N][H][W][cout] layout) from the values computed here
+      // anyway, so that weight gradient runs without re-applying the GroupNorm + SiLU on load
+      const bool wact = g.act != nullptr;
+      const rsrc_t rac = mkrsrc(wact ? g.act + (size_t)t.n0 * p.H * p.W * p.cout : p.bias);
+      const int vba = vbase(t);
 #pragma unroll
       for (int nr = 0; nr < 2; ++nr) {
         // the per-(image, channel) GroupNorm parameters, loaded during the unit's last chunks (gnb_params)
@@ -846,10 +852,15 @@ __device__ __forceinline__ void conv_x3_body(const ConvParams& p, const GnbParam
             const float nrm = xhat * gam + bet;
             const float zz = nrm * onep[nr] + sh;
             float dz = acc[mr][nr][r];
+            float av = zz;
             if (g.silu) {
               const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zz * -1.4426950408889634f));
               dz = dz * (sg * (1.0f + zz * (1.0f - sg)));
+              av = zz * sg;
             }
+            if (wact)
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, av), rac, vba + mr * mstep + nr * 128,
+                                                    roff(r), X3_STORE_AUX);
             s1 += dz;
             s2 += dz * nrm;
             s3 += dz * xhat;

@@ -2829,11 +2829,11 @@ int64_t ifd_tr_gnb_part_floats(int N, int H, int cout) {
   return (int64_t)N * (HW >= 64 ? HW / 64 : 1) * cout * 3;
 }
 
-int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, const float* bias, int cin_pad,
-                       int cout, float* out, float* part, int64_t part_floats, unsigned* guard, const float* gx0, int gc0,
-                       const float* gx1, const float* stats, const float* gamma, const float* beta, const float* ss,
-                       int ss_stride, int act_silu, float* gpart, int64_t gpart_floats, int* gpart_nsl, int nprod,
-                       void* stream) {
+int ifd_tr_conv_x3_gnb_act(const float* dy, int cdy, int N, int H, const void* wx3, const float* bias, int cin_pad,
+                           int cout, float* out, float* part, int64_t part_floats, unsigned* guard, const float* gx0,
+                           int gc0, const float* gx1, const float* stats, const float* gamma, const float* beta,
+                           const float* ss, int ss_stride, int act_silu, float* gpart, int64_t gpart_floats,
+                           int* gpart_nsl, float* act_out, int nprod, void* stream) {
   if (!gpart_nsl || !gx0 || !stats || !gamma || !beta || gc0 <= 0 || gc0 > cout || (gc0 < cout && !gx1) ||
       cout % 32 || ifd_tr_gnb_part_floats(N, H, cout) > gpart_floats || !gpart) {
     set_error("ifd_tr_conv_x3_gnb: bad GroupNorm arguments or partial-sum buffer too small");
@@ -2844,8 +2844,19 @@ int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, 
   g.stats = stats; g.gamma = gamma; g.beta = beta;
   g.ss = ss; g.ss_stride = ss_stride; g.silu = act_silu;
   g.part = gpart;
+  g.act = act_out;
   return conv_x3_run(dy, cdy, nullptr, 0, N, H, wx3, bias, cin_pad, cout, nullptr, out, part, part_floats, guard, 9,
                      nullptr, 0, nullptr, nullptr, nprod, stream, nullptr, nullptr, &g, gpart_nsl);
+}
+
+int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, const float* bias, int cin_pad,
+                       int cout, float* out, float* part, int64_t part_floats, unsigned* guard, const float* gx0, int gc0,
+                       const float* gx1, const float* stats, const float* gamma, const float* beta, const float* ss,
+                       int ss_stride, int act_silu, float* gpart, int64_t gpart_floats, int* gpart_nsl, int nprod,
+                       void* stream) {
+  return ifd_tr_conv_x3_gnb_act(dy, cdy, N, H, wx3, bias, cin_pad, cout, out, part, part_floats, guard, gx0, gc0, gx1,
+                                stats, gamma, beta, ss, ss_stride, act_silu, gpart, gpart_floats, gpart_nsl, nullptr,
+                                nprod, stream);
 }
 
 // 1x1 conv (forward, or transpose = 1: the dgrad W^T) on the sampler's dedicated split 1x1 kernel (skip_x3.hip,

@@ -58,6 +58,8 @@ TRAIN_EXPORTS = {
     "ifd_tr_gnb_part_floats": (i64, [i32, i32, i32]),
     "ifd_tr_conv_x3_gnb": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp, vp, vp, vp, i32,
                                  i32, vp, i64, _c.POINTER(i32), i32, vp]),
+    "ifd_tr_conv_x3_gnb_act": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp, vp, vp, vp,
+                                     i32, i32, vp, i64, _c.POINTER(i32), vp, i32, vp]),
     "ifd_tr_gn_bwd_from_part": (i32, [vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, i32, vp, vp,
                                       vp, vp, i64, vp, i32, vp, vp]),
     "ifd_tr_gn_coef": (i32, [vp, i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, i32, f32, vp, vp, vp, vp, i64, vp]),
@@ -149,13 +151,20 @@ class UNetTrainer:
 
     fuse_gnb (split modes): the dgrad conv whose output feeds a GroupNorm backward (ResBlock out_layers.3 ->
     out_layers.0, in_layers.2 -> in_layers.0 without resampling) computes that backward's pass-1 partial sums in
-    its epilogue (ifd_tr_conv_x3_gnb): the pass over (dout, x) of ifd_tr_gn_bwd is not run."""
+    its epilogue (ifd_tr_conv_x3_gnb): the pass over (dout, x) of ifd_tr_gn_bwd is not run.
+
+    gnb_act (with fuse_gnb, round 6, off by default): that epilogue also writes the GroupNorm's forward output
+    silu(z) — the input of the conv whose weight gradient is next (ifd_tr_conv_x3_gnb_act) — so that weight
+    gradient runs the plain split kernel on it instead of re-applying GroupNorm + SiLU on load (1.82 vs 1.66 ms
+    at the 256^2 128 -> 128 layer alone, profiles/r06e); the dgrad then runs first. Measured in the whole step
+    it is a wash (profiles/r06g): the weight gradients gain 0.85 ms per step, the GNB dgrads lose 0.95 ms to the
+    extra stores (242.7 / 243.6 vs 243.4 / 242.9 images/s off / on)."""
 
     SPLIT_MODES = ("3xf16", "f16")
 
     def __init__(self, cfg: UNetConfig = FULL, device="cuda", lr=5e-5, weight_decay=0.01, betas=(0.9, 0.999),
                  eps=1e-8, max_norm=1.0, precision="fp32", x3_dgrad=True, x3_wgrad=True, x3_loss_scale_log2=20,
-                 fuse_gn=True, fuse_gnb=True):
+                 fuse_gn=True, fuse_gnb=True, gnb_act=False):
         if precision not in ("fp32", "3xf16", "f16"):
             raise ValueError(f"precision must be 'fp32', '3xf16' or 'f16', got {precision!r}")
         self.precision = precision
@@ -164,6 +173,7 @@ class UNetTrainer:
         self.x3_loss_scale_log2 = int(x3_loss_scale_log2)
         self.fuse_gn = bool(fuse_gn)
         self.fuse_gnb = bool(fuse_gnb)
+        self.gnb_act = bool(gnb_act)
         self.guard_trips = 0
         self.cfg = cfg
         self.dev = torch.device(device)
@@ -583,12 +593,14 @@ class UNetTrainer:
         return dx, None, True
 
     def dgrad_gn_bwd(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx=None, ss=None, ss_stride=0, dss=None,
-                     silu=True, x1=None, C0=None, add=None, split=None):
+                     silu=True, x1=None, C0=None, add=None, split=None, act_sink=None):
         """gn_bwd(conv^T(dy)) - the dgrad of conv `wname` fed into the GroupNorm backward of its input x (C
         channels; x1 / C0 as gn_bwd). On the split kernel the GroupNorm's pass 1 runs in the dgrad's epilogue
-        (ifd_tr_conv_x3_gnb); shapes it does not take run conv() then gn_bwd()."""
+        (ifd_tr_conv_x3_gnb); shapes it does not take run conv() then gn_bwd(). act_sink (a list): on the fused
+        path the epilogue also writes the GroupNorm's forward output silu(GN(x)(1 + s) + shift), [N, H, H, C], and
+        appends it (round 6: the next weight gradient then reads it instead of re-applying GN + SiLU on load)."""
         out = self._dgrad_gnb(dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0, add,
-                              split)
+                              split, act_sink)
         if out is not None:
             return out
         da = self.conv(dy, cdy, N, H, wname, transpose=True)
@@ -596,7 +608,7 @@ class UNetTrainer:
                            x1=x1, C0=C0, add=add, split=split)
 
     def _dgrad_gnb(self, dy, cdy, N, H, wname, x, C, prefix, stats, dx, ss, ss_stride, dss, silu, x1, C0, add=None,
-                   split=None):
+                   split=None, act_sink=None):
         if not (self.fuse_gnb and self._x3_active(True)):
             return None
         w = self.p(wname)
@@ -618,12 +630,15 @@ class UNetTrainer:
         nsl = _c.c_int(0)
         c0 = C0 if x1 is not None else C
         gam, bet = self.p(prefix + "weight"), self.p(prefix + "bias")
-        rc = lib().ifd_tr_conv_x3_gnb(P(dy), cdy, N, H, P(wx3), P(self._zero_bias), cdy, cin, P(da), P(part), pf,
-                                      P(self._guard), P(x), c0, P(x1), P(stats), P(gam), P(bet), P(ss), ss_stride,
-                                      int(silu), P(gpart), gpf, _c.byref(nsl), self._nprod(), self.s)
+        act = self._empty(N, H, H, cin) if act_sink is not None and self.gnb_act else None
+        rc = lib().ifd_tr_conv_x3_gnb_act(P(dy), cdy, N, H, P(wx3), P(self._zero_bias), cdy, cin, P(da), P(part), pf,
+                                          P(self._guard), P(x), c0, P(x1), P(stats), P(gam), P(bet), P(ss), ss_stride,
+                                          int(silu), P(gpart), gpf, _c.byref(nsl), P(act), self._nprod(), self.s)
         if rc == 3:
             return None
         chk(rc)
+        if act is not None and nsl.value > 0:
+            act_sink.append(act)
         if nsl.value == 0:  # (the conv ran; its geometry could not carry the partial sums)
             return self.gn_bwd(da, x, N, H * H, C, prefix, stats, dx=dx, ss=ss, ss_stride=ss_stride, dss=dss,
                                silu=silu, x1=x1, C0=C0, add=add, split=split)
@@ -932,23 +947,32 @@ class UNetTrainer:
             return dx, r
         sv = saved[p]
         cin, cout, mode, r, ro = L["cin"], L["cout"], sv["mode"], sv["r"], sv["ro"]
-        # h2 = conv2(a2) + b2; out = skip + h2
-        if sv["g2"] is not None:
+        # h2 = conv2(a2) + b2; out = skip + h2. The dgrad first: its GNB epilogue can write a2 itself (act2), which
+        # the weight gradient then reads instead of re-applying GroupNorm + scale/shift + SiLU to h1 on load
+        dE = self._zeros(N, 2 * cout)
+        act2 = []
+        dh1 = self.dgrad_gn_bwd(dout, cout, N, ro, p + "out_layers.3.weight", sv["h1"], cout, p + "out_layers.0.",
+                                sv["st2"], ss=sv["E"], ss_stride=2 * cout, dss=dE, silu=True,
+                                act_sink=act2 if sv["g2"] is not None else None)
+        if act2:
+            self.wgrad(dout, cout, act2[0], cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias")
+        elif sv["g2"] is not None:
             self.wgrad(dout, cout, sv["h1"], cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias",
                        gn=sv["g2"])
         else:
             self.wgrad(dout, cout, sv["a2"], cout, N, ro, p + "out_layers.3.weight", p + "out_layers.3.bias")
-        dE = self._zeros(N, 2 * cout)
-        dh1 = self.dgrad_gn_bwd(dout, cout, N, ro, p + "out_layers.3.weight", sv["h1"], cout, p + "out_layers.0.",
-                                sv["st2"], ss=sv["E"], ss_stride=2 * cout, dss=dE, silu=True)
+        del act2
         self.linear_bwd(dE, self._tape["emb"], N, p + "emb_layers.1.weight", p + "emb_layers.1.bias", pre_silu=True,
                         dx=demb)
         x1, c1 = sv.get("x1"), sv.get("c1", 0)
         c0 = cin - c1  # (x1: the block input is concat(x[c0], x1[c1]), never materialised)
-        if sv["g1"] is not None:
+        # without resampling, conv1's weight gradient waits for the dgrad below: its GNB epilogue can write
+        # a1 = silu(GN1(x)) for it (act1), instead of the weight gradient re-applying GN + SiLU to x on load
+        defer1 = sv["g1"] is not None and not mode
+        if sv["g1"] is not None and not defer1:
             self.wgrad(dh1, cout, sv["x"], c0, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias", gn=sv["g1"],
                        x1=x1, c1=c1)
-        else:
+        elif sv["g1"] is None:
             self.wgrad(dh1, cout, sv["a1r"], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
         if mode:
             da1r = self.conv(dh1, cout, N, ro, p + "in_layers.2.weight", transpose=True)
@@ -973,16 +997,23 @@ class UNetTrainer:
             # the skip path's gradient (dout itself, or the 1x1 conv's fresh dgrad) is the accumulation
             # target of the GroupNorm input gradient: no separate add pass; the dgrad of in_layers.2 carries
             # the GroupNorm backward's pass 1 (dgrad_gn_bwd)
+            act1 = [] if defer1 else None
             if split and x1 is not None:
                 # the skip path's gradient joins as the addend and dx comes out per concat source
                 if add is not None:
                     raise ValueError("a split input gradient takes no other addend")
                 pair = (self._empty(N, r, r, c0), self._empty(N, r, r, c1))
                 dx = self.dgrad_gn_bwd(dh1, cout, N, ro, p + "in_layers.2.weight", sv["x"], cin, p + "in_layers.0.",
-                                       sv["st1"], silu=True, x1=x1, C0=c0, add=(dxr, cin, 0), split=pair)
+                                       sv["st1"], silu=True, x1=x1, C0=c0, add=(dxr, cin, 0), split=pair,
+                                       act_sink=act1)
             else:
                 dx = self.dgrad_gn_bwd(dh1, cout, N, ro, p + "in_layers.2.weight", sv["x"], cin, p + "in_layers.0.",
-                                       sv["st1"], dx=dxr, silu=True, x1=x1, C0=c0, add=add)
+                                       sv["st1"], dx=dxr, silu=True, x1=x1, C0=c0, add=add, act_sink=act1)
+            if act1:
+                self.wgrad(dh1, cout, act1[0], cin, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias")
+            elif defer1:
+                self.wgrad(dh1, cout, sv["x"], c0, N, ro, p + "in_layers.2.weight", p + "in_layers.2.bias",
+                           gn=sv["g1"], x1=x1, c1=c1)
         return dx, r
 
     # ------------------------------------------------------------------ loss / step

@@ -179,6 +179,16 @@ int ifd_tr_conv_x3_gnb(const float* dy, int cdy, int N, int H, const void* wx3, 
                        const float* gx1, const float* stats, const float* gamma, const float* beta, const float* ss,
                        int ss_stride, int act_silu, float* gpart, int64_t gpart_floats, int* gpart_nsl, int nprod,
                        void* stream);
+/* The same, and when act_out is non-null (and the geometry fuses, *gpart_nsl > 0) the epilogue also writes the
+ * GroupNorm's forward output act = silu(z) (z without act_silu), z = GN(x) (1 + s) + shift, to act_out
+ * [N][H][W][cout] - the input of the conv whose weight gradient comes next (round 6), from the values the pass-1
+ * sums compute anyway, so that weight gradient need not re-apply the GroupNorm + SiLU on load
+ * (ifd_tr_conv_wgrad_x3 on act_out instead of ifd_tr_conv_wgrad_x3_gn on x). */
+int ifd_tr_conv_x3_gnb_act(const float* dy, int cdy, int N, int H, const void* wx3, const float* bias, int cin_pad,
+                           int cout, float* out, float* part, int64_t part_floats, unsigned* guard, const float* gx0,
+                           int gc0, const float* gx1, const float* stats, const float* gamma, const float* beta,
+                           const float* ss, int ss_stride, int act_silu, float* gpart, int64_t gpart_floats,
+                           int* gpart_nsl, float* act_out, int nprod, void* stream);
 /* ifd_tr_gn_bwd_cat with pass 1 done (gpart from ifd_tr_conv_x3_gnb): reduce, group, parameter and dx passes
  * (add, dx1 as there). work: N*C*3 + N*64 floats. */
 int ifd_tr_gn_bwd_from_part(const float* dout, const float* x0, int C0, const float* x1, int N, int HW, int C,

@@ -448,3 +448,62 @@ def test_conv1x1_x3_vs_fp64(N, H, c0, c1, cout, transpose, record):
     err = float((out.double() - ref).abs().max())
     record(f"train_fuse/conv1x1_x3/{N}x{H}x{c0}+{c1}->{co}/t{transpose}", maxabs=err)
     assert err <= 2e-6 * float(ref.abs().max()), err
+
+
+@pytest.mark.parametrize("N,H,cdy,C,C0,use_ss", [(8, 64, 128, 128, 128, True), (16, 32, 128, 256, 128, False)])
+def test_conv_x3_gnb_act_output(N, H, cdy, C, C0, use_ss, record):
+    """ifd_tr_conv_x3_gnb_act (round 6): the GNB dgrad's epilogue also writes the GroupNorm's forward output
+    act = silu(GN(x) (1 + s) + shift) over every pixel and channel, against a float64 restatement from the same
+    statistics (the epilogue's arithmetic rounds per step: max |d| <= 1e-5 max|ref|); the dgrad output and the
+    partial sums equal the plain entry's bit for bit."""
+    from ifd import _lib
+    from ifd.train import P, chk, lib
+
+    s = _lib.stream_ptr(DEV)
+    g = torch.Generator().manual_seed(N * H + C + 1)
+    dy = torch.randn(N, H, H, cdy, generator=g).to(DEV)
+    w = (torch.randn(cdy, C, 3, 3, generator=g) / (3 * C ** 0.5)).to(DEV)
+    x = (torch.randn(N, H, H, C, generator=g) + 0.2).to(DEV)
+    x0, x1 = x[..., :C0].contiguous(), (x[..., C0:].contiguous() if C0 < C else None)
+    gam = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    ss = (0.1 * torch.randn(N, 2 * C, generator=g)).to(DEV) if use_ss else None
+    st = torch.empty(N * 64, device=DEV)
+    nsl0 = lib().ifd_tr_gn_slices(H * H, N, C)
+    work = torch.empty(N * nsl0 * 64, device=DEV, dtype=torch.float64)
+    gout = torch.empty(N, H * H, C, device=DEV)
+    chk(lib().ifd_tr_gn_fwd(P(x), N, H * H, C, P(gam), P(bet), P(ss), 2 * C if use_ss else 0, 1, P(gout), P(st),
+                            P(work), work.numel(), s))
+    wx3 = torch.empty(C * cdy * 9, device=DEV)
+    guard = torch.zeros(4, device=DEV, dtype=torch.int32)
+    chk(lib().ifd_tr_pack_conv_x3(P(w), cdy, C, 9, cdy, C, 1, P(wx3), P(guard), s))
+    zb = torch.zeros(4096, device=DEV)
+    pf = lib().ifd_tr_conv_x3_part_floats(N, H, cdy, C)
+    part = torch.empty(max(pf, 1), device=DEV)
+    gpf = lib().ifd_tr_gnb_part_floats(N, H, C)
+    outs = []
+    for with_act in (False, True):
+        da = torch.empty(N, H, H, C, device=DEV)
+        gpart = torch.empty(gpf, device=DEV)
+        act = torch.full((N, H, H, C), float("nan"), device=DEV) if with_act else None
+        nsl = ctypes.c_int(0)
+        chk(lib().ifd_tr_conv_x3_gnb_act(P(dy), cdy, N, H, P(wx3), P(zb), cdy, C, P(da), P(part), pf, P(guard), P(x0),
+                                         C0, P(x1), P(st), P(gam), P(bet), P(ss), 2 * C if use_ss else 0, 1, P(gpart),
+                                         gpf, ctypes.byref(nsl), P(act), 3, s))
+        assert nsl.value > 0
+        outs.append((da, gpart, act))
+    torch.cuda.synchronize()
+    (da0, gp0, _), (da1, gp1, act) = outs
+    assert torch.equal(da0, da1) and torch.equal(gp0, gp1)
+    stc = st.view(N, 32, 2).double().cpu()
+    xd = x.double().cpu().view(N, H * H, 32, C // 32)
+    xhat = (xd - stc[:, None, :, 0:1]) * stc[:, None, :, 1:2]
+    z = xhat.view(N, H * H, C) * gam.double().cpu() + bet.double().cpu()
+    if use_ss:
+        sd = ss.double().cpu()
+        z = z * (1 + sd[:, None, :C]) + sd[:, None, C:]
+    ref = (z * torch.sigmoid(z)).view(N, H, H, C)
+    err = float((act.double().cpu() - ref).abs().max())
+    record(f"train_fuse/gnb_act/{N}x{H}x{C}", maxabs=err, ref_max=float(ref.abs().max()))
+    assert torch.isfinite(act).all()
+    assert err <= 1e-5 * float(ref.abs().max()), err
