@@ -180,7 +180,9 @@ int ifd_ddpm_step(ifd_handle* h, const int64_t* t, int64_t B, int H, int W, floa
 static int update_common(int mode, const float* out6, int64_t B, int H, int W, float* img, const float* gt,
                          const float* mask, const float* noise, const float* known, const ifd_step_coeffs* c,
                          void* stream) {
-  if (!out6 || !img || !c) { set_error("ifd update: null argument"); return 2; }
+  if (B < 0 || H <= 0 || W <= 0 || !c) { set_error("ifd update: bad shape or null coefficients"); return 2; }
+  if (B == 0) return 0;  /* an empty batch: nothing to launch (a zero-size grid is a launch error) */
+  if (!out6 || !img) { set_error("ifd update: null argument"); return 2; }
   if (c->inject && (!gt || !mask || !known)) { set_error("ifd update: inject requires gt, mask, known"); return 2; }
   if ((mode == ifd::EPI_DDPM || c->use_noise) && !noise) { set_error("ifd update: noise required"); return 2; }
   ifd::StepCoeffs sc;
@@ -201,6 +203,8 @@ int ifd_ddpm_update(const float* out6, int64_t B, int H, int W, float* img, cons
 
 int ifd_blend(const float* result, const float* gt, const float* mask, int64_t B, int C, int H, int W, float* out,
               void* stream) {
+  if (B < 0 || C <= 0 || H <= 0 || W <= 0) { set_error("ifd_blend: bad shape"); return 2; }
+  if (B == 0) return 0;  /* an empty batch: nothing to launch */
   if (!result || !gt || !mask || !out) { set_error("ifd_blend: null argument"); return 2; }
   ifd::launch_blend(result, gt, mask, out, (int)B, C, H * W, (hipStream_t)stream);
   return IFD_LAUNCH_STATUS() ? 1 : 0;

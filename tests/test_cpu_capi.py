@@ -148,3 +148,16 @@ def test_check_reports_then_clears_the_message():
     rc = L.ifd_tr_scale(None, 4, 1.0, None)
     with pytest.raises(RuntimeError, match="ifd_tr_scale: bad arguments"):
         _lib.check(rc)
+
+
+def test_empty_batches_are_no_ops():
+    """The elementwise entry points take an empty batch as a no-op (as torch does on empty tensors) instead of
+    launching a zero-size grid, which HIP reports as a launch error; no GPU is touched."""
+    from ifd import _lib
+    L = _lib.lib()
+    c = _lib.StepCoeffs()
+    assert L.ifd_blend(None, None, None, 0, 3, 8, 8, None, None) == 0
+    assert L.ifd_ddim_update(None, 0, 8, 8, None, None, None, None, None, ctypes.byref(c), None) == 0
+    assert L.ifd_ddpm_update(None, 0, 8, 8, None, None, None, None, None, ctypes.byref(c), None) == 0
+    assert L.ifd_to_u8(None, 0, 3, 8, 8, None, None) == 0
+    assert L.ifd_blend(None, None, None, -1, 3, 8, 8, None, None) != 0
