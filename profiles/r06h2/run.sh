@@ -2,7 +2,7 @@
 # round 6 session h: the final library (after the gnb_act entry point; rerun as h2 after the empty-batch entry checks) - every GPU test, smoke, the default bench line
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r06h; mkdir -p $O
+O=$R/gpurun_out/r06h2; mkdir -p $O
 cd $R
 PYTEST_X= bash tools/gpu_tests.sh; rc=$?; cp gpurun_out/gpu_tests.txt gpurun_out/parity.json $O/; echo "tests rc=$rc"
 grep -E "^FAILED|passed|failed" $O/gpu_tests.txt | tail -4
